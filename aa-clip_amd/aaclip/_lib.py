@@ -1,0 +1,77 @@
+"""ctypes binding of libaaclip_hip.so (C ABI: include/aaclip.h).
+
+The product path has NO CPU fallback: if the library is missing or a call
+fails, this raises. Build it with `python __graft_entry__.py` (build()) or
+`make -C aa-clip_amd/csrc`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaaclip_hip.so")
+ABI_VERSION = 1
+
+F32 = 0
+BF16 = 1
+EPI_BIAS = 1
+EPI_GELU = 2
+EPI_LEAKY = 4
+EPI_RESID = 8
+EPI_AUX_BF16 = 16
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_F = ctypes.c_float
+
+# name -> argtypes (restype int unless noted); mirrors include/aaclip.h
+SIGNATURES = {
+    "aaclip_abi_version": [],
+    "aaclip_arch": [],
+    "aaclip_gemm": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _I, _P, _P, _L, _P, _L, _I, _I, _I, _P],
+    "aaclip_attention": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aaclip_im2col": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aaclip_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "aaclip_block_tail": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "aaclip_layernorm": [_I, _P, _L, _P, _P, _P, _L, _I, _I, _P],
+    "aaclip_text_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "aaclip_eot_ln": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "aaclip_anchor_reduce": [_P, _I, _I, _P, _I, _I, _P],
+    "aaclip_l2_normalize": [_I, _I, _P, _L, _P, _L, _I, _I, _P],
+    "aaclip_patch_scores": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _P, _P],
+    "aaclip_blur_upsample": [_P, _P, _I, _I, _I, _I, _I, _F, _I, _P],
+    "aaclip_anomaly_map": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P],
+    "aaclip_image_score": [_I, _P, _L, _P, _I, _I, _I, _I, _P, _P, _P, _P],
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: the HIP kernels are not built "
+                "(run `python __graft_entry__.py` or `make -C aa-clip_amd/csrc`). "
+                "There is no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_char_p if name == "aaclip_arch" else ctypes.c_int
+        if handle.aaclip_abi_version() != ABI_VERSION:
+            raise RuntimeError("libaaclip_hip.so ABI version mismatch; rebuild it")
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        kind = "bad argument" if rc == 1 else f"launch failed (hipError {rc - 1000})"
+        raise RuntimeError(f"{name}: {kind} (rc={rc})")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)

@@ -1,0 +1,279 @@
+"""Device-side execution of AA-CLIP's inference path on libaaclip_hip.so.
+
+VisualEngine = AdaptedCLIP.forward (reference model/adapter.py:67-112) +
+the anomaly map / image score of test.py:80-93; TextEngine =
+AdaptedCLIP.encode_text / CLIP.encode_text (adapter.py:114-145,
+model/model.py:190-201) + the prompt-ensemble anchors (forward_utils.py:138-162).
+
+Data layout in HBM (token-major "NLD", one row per token):
+  x      fp32 [B*(P+1), 1024]   residual stream (kept fp32 across all 24 blocks)
+  h      cdt  [B*(P+1), 1024]   LayerNorm output feeding the next GEMM
+  qkv    cdt  [B*(P+1), 3072]   packed [q|k|v] (nn.MultiheadAttention in_proj order)
+  attn   cdt  [B*(P+1), 1024]   merged heads
+  fc     cdt  [B*(P+1), 4096]   GELU(c_fc)
+  xb     bf16 [B*(P+1), 1024]   bf16 copy of x written by the c_proj epilogue (adapter input)
+  u      fp32 [B*(P+1), 1024]   LeakyReLU(adapter(x))
+  tap_l  cdt  [B*P, 1024]       ln_post(x[:, 1:]) at each level
+  seg    cdt  [B*P, (L+1)*768]  seg_proj of level l in cols l*768.., det_proj in cols L*768..
+cdt = compute dtype: bf16 (MFMA bf16, perf path) or fp32 (fp32 MFMA, parity mode).
+Weights are packed once: nn.Linear [N,K] layout kept (the GEMM is A.W^T);
+conv1 flattened to [1024, 640] (K padded 588 -> 640 with zeros).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+WIDTH = 1024
+HEADS = 16
+LAYERS = 24
+PATCH = 14
+EMBED = 768
+KPATCH = 640  # 3*14*14 = 588 padded to a multiple of 64
+DOMAIN_BLUR = {"Industrial": (7, 1.0), "Medical": (9, 1.5)}
+
+
+def _blur_for(domain: str):
+    # forward_utils.py:205-206: Industrial k=7 sigma=1, anything else k=9 sigma=1.5
+    return DOMAIN_BLUR["Industrial"] if domain == "Industrial" else DOMAIN_BLUR["Medical"]
+
+
+def _proj_weight(ad: dict, prefix: str):
+    if prefix + ".fc.0.weight" in ad:
+        return ad[prefix + ".fc.0.weight"], True
+    return ad[prefix + ".fc.weight"], False
+
+
+class VisualEngine:
+    def __init__(self, vparams: dict, adapter: dict, *, levels=(6, 12, 18, 24), image_adapt_until=6,
+                 image_adapt_weight=0.1, dtype=torch.bfloat16):
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("dtype must be bfloat16 or float32")
+        self.dtype = dtype
+        self.levels = list(levels)
+        self.adapt_until = int(image_adapt_until)
+        self.i_w = float(image_adapt_weight)
+        if len(self.levels) > 8 or sorted(self.levels) != self.levels or self.levels[-1] > LAYERS:
+            raise ValueError("levels must be sorted block indices in 1..24 (at most 8)")
+        dev = vparams["visual.conv1.weight"].device
+        if dev.type != "cuda":
+            raise RuntimeError("VisualEngine needs device tensors (no CPU path)")
+        self.device = dev
+        f32 = lambda t: t.detach().to(dev, torch.float32).contiguous()  # noqa: E731
+        cdt = lambda t: t.detach().to(dev, dtype).contiguous()  # noqa: E731
+        w = vparams["visual.conv1.weight"].detach().reshape(WIDTH, -1)
+        conv = torch.zeros(WIDTH, KPATCH, device=dev, dtype=torch.float32)
+        conv[:, : w.shape[1]] = w
+        self.conv = conv.to(dtype).contiguous()
+        self.cls = f32(vparams["visual.class_embedding"])
+        self.pos = f32(vparams["visual.positional_embedding"])
+        self.ln_pre = (f32(vparams["visual.ln_pre.weight"]), f32(vparams["visual.ln_pre.bias"]))
+        self.ln_post = (f32(vparams["visual.ln_post.weight"]), f32(vparams["visual.ln_post.bias"]))
+        self.blocks = []
+        for i in range(LAYERS):
+            p = f"visual.transformer.resblocks.{i}."
+            self.blocks.append(dict(
+                ln1=(f32(vparams[p + "ln_1.weight"]), f32(vparams[p + "ln_1.bias"])),
+                ln2=(f32(vparams[p + "ln_2.weight"]), f32(vparams[p + "ln_2.bias"])),
+                w_qkv=cdt(vparams[p + "attn.in_proj_weight"]), b_qkv=f32(vparams[p + "attn.in_proj_bias"]),
+                w_o=cdt(vparams[p + "attn.out_proj.weight"]), b_o=f32(vparams[p + "attn.out_proj.bias"]),
+                w_fc=cdt(vparams[p + "mlp.c_fc.weight"]), b_fc=f32(vparams[p + "mlp.c_fc.bias"]),
+                w_pr=cdt(vparams[p + "mlp.c_proj.weight"]), b_pr=f32(vparams[p + "mlp.c_proj.bias"]),
+            ))
+        self.w_adapt = [cdt(adapter[f"layer_adapters.{i}.fc.0.weight"]) for i in range(self.adapt_until)]
+        self.w_seg, relus = [], []
+        for i in range(len(self.levels)):
+            wt, r = _proj_weight(adapter, f"seg_proj.{i}")
+            self.w_seg.append(wt)
+            relus.append(r)
+        w_det, r_det = _proj_weight(adapter, "det_proj")
+        if len(set(relus + [r_det])) != 1:
+            raise ValueError("seg_proj/det_proj relu variants must agree")
+        self.relu = r_det
+        self.w_seg = [cdt(t) for t in self.w_seg[:-1]] + [cdt(torch.cat([self.w_seg[-1], w_det], 0))]
+        self._ws = {}
+
+    # ------------------------------------------------------------------ workspace
+    def _workspace(self, B: int, S: int):
+        key = (B, S)
+        if key in self._ws:
+            return self._ws[key]
+        g = S // PATCH
+        P = g * g
+        n_tok = P + 1
+        if self.pos.shape[0] != n_tok:
+            raise ValueError(f"positional embedding has {self.pos.shape[0]} rows, image needs {n_tok} "
+                             "(resize it at load time, reference model/model.py:395-426)")
+        R = B * n_tok
+        dev, cdt = self.device, self.dtype
+        e = lambda *s, dt=cdt: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+        L = len(self.levels)
+        ws = dict(
+            g=g, P=P, n_tok=n_tok,
+            cols=e(B * P, KPATCH), x=e(R, WIDTH, dt=torch.float32), h=e(R, WIDTH), qkv=e(R, 3 * WIDTH),
+            attn=e(R, WIDTH), fc=e(R, 4 * WIDTH), u=e(R, WIDTH, dt=torch.float32),
+            xb=e(R, WIDTH, dt=torch.bfloat16) if cdt == torch.bfloat16 else None,
+            taps=[e(B * P, WIDTH) for _ in range(L)],
+            # all level projections + det in one [B*P, (L+1)*768] buffer: level l at
+            # columns l*768, det_proj at L*768 (one row stride for the map kernel)
+            segbuf=e(B * P, (L + 1) * EMBED),
+            grid=e(B * P, dt=torch.float32), partial=e(B * ((P + 63) // 64) * EMBED, dt=torch.float32),
+            det=e(B, EMBED, dt=torch.float32), score=e(B, dt=torch.float32),
+            map=e(B, S, S, dt=torch.float32),
+        )
+        self._ws = {key: ws}  # keep one batch shape resident
+        return ws
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def forward_raw(self, x: torch.Tensor):
+        """Run the visual tower; returns (seg_raw list of [B*P, 768] views,
+        det_raw [B*P, 768] view, workspace). Rows are unnormalised projections."""
+        if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != x.shape[3] or x.shape[2] % PATCH:
+            raise ValueError("input must be [B, 3, S, S] with S a multiple of 14")
+        x = x.to(self.device, torch.float32).contiguous()
+        B, _, S, _ = x.shape
+        ws = self._workspace(B, S)
+        P, n_tok = ws["P"], ws["n_tok"]
+        X, H = ws["x"], ws["h"]
+        ops.im2col(x, ws["cols"], PATCH)
+        ops.gemm(ws["cols"], self.conv, X, row_group=P, row_group_out=n_tok, row_offset=1)
+        ops.embed_ln(X, self.cls, self.pos, self.ln_pre, self.blocks[0]["ln1"], H, B, n_tok)
+        lvl = {lv: j for j, lv in enumerate(self.levels)}
+        last = self.levels[-1]
+        for i in range(last):
+            blk = self.blocks[i]
+            ops.gemm(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
+            ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS)
+            ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
+            ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], H)
+            ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True)
+            adapt = i < self.adapt_until
+            ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X,
+                     aux=ws["xb"] if (adapt and ws["xb"] is not None) else None)
+            tap = ws["taps"][lvl[i + 1]] if (i + 1) in lvl else None
+            nxt = self.blocks[i + 1]["ln1"] if i + 1 < last else None
+            u = None
+            if adapt:
+                ops.gemm(ws["xb"] if ws["xb"] is not None else X, self.w_adapt[i], ws["u"], leaky=True)
+                u = ws["u"]
+            if u is not None or nxt is not None or tap is not None:
+                ops.block_tail(X, n_tok, u=u, adapt_weight=self.i_w, ln=nxt, h=H if nxt else None,
+                               post=self.ln_post, tap=tap)
+        L = len(self.levels)
+        sb = ws["segbuf"]
+        for j in range(L):
+            ncol = self.w_seg[j].shape[0]
+            ops.gemm(ws["taps"][j], self.w_seg[j], sb[:, j * EMBED:j * EMBED + ncol], leaky=self.relu)
+        seg = [sb[:, j * EMBED:(j + 1) * EMBED] for j in range(L)]
+        det = sb[:, L * EMBED:]
+        return seg, det, ws
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor):
+        """AdaptedCLIP.forward contract: (list[L] of [B,P,768] unit rows, det [B,768]) fp32."""
+        seg_raw, det_raw, ws = self.forward_raw(x)
+        B = x.shape[0]
+        P = ws["P"]
+        out = []
+        for s in seg_raw:
+            y = torch.empty(B * P, EMBED, device=self.device, dtype=torch.float32)
+            ops.l2_normalize(s, y)
+            out.append(y.view(B, P, EMBED))
+        det = torch.empty(B, EMBED, device=self.device, dtype=torch.float32)
+        ops.image_score(det_raw, B, P, ws["partial"], det=det)
+        return out, det
+
+    @torch.no_grad()
+    def predict(self, x: torch.Tensor, T: torch.Tensor, domain: str = "Industrial"):
+        """Fused test path: (anomaly map [B,S,S] fp32, image score [B] fp32),
+        = test.py:80-93 with the level sum ahead of blur+upsample."""
+        seg_raw, det_raw, ws = self.forward_raw(x)
+        B, S = x.shape[0], x.shape[-1]
+        T = T.to(self.device, torch.float32).contiguous()
+        k, s = _blur_for(domain)
+        ops.anomaly_map(seg_raw, T, ws["map"], ws["grid"], g=ws["g"], ksize=k, sigma=s)
+        ops.image_score(det_raw, B, ws["P"], ws["partial"], det=ws["det"], T=T, score=ws["score"])
+        return ws["map"], ws["score"]
+
+
+class TextEngine:
+    """12-block causal text tower; adapted (text_adapter) or plain CLIP projection."""
+
+    def __init__(self, params: dict, text_adapter: dict | None, *, text_adapt_until=3, text_adapt_weight=0.1,
+                 dtype=torch.float32):
+        dev = params["token_embedding.weight"].device
+        if dev.type != "cuda":
+            raise RuntimeError("TextEngine needs device tensors (no CPU path)")
+        self.device, self.dtype = dev, dtype
+        f32 = lambda t: t.detach().to(dev, torch.float32).contiguous()  # noqa: E731
+        cdt = lambda t: t.detach().to(dev, dtype).contiguous()  # noqa: E731
+        self.width = params["ln_final.weight"].shape[0]
+        self.heads = self.width // 64
+        self.tok_emb = f32(params["token_embedding.weight"])
+        self.pos = f32(params["positional_embedding"])
+        self.ln_final = (f32(params["ln_final.weight"]), f32(params["ln_final.bias"]))
+        nl = len({k.split(".")[2] for k in params if k.startswith("transformer.resblocks.")})
+        self.blocks = []
+        for i in range(nl):
+            p = f"transformer.resblocks.{i}."
+            self.blocks.append(dict(
+                ln1=(f32(params[p + "ln_1.weight"]), f32(params[p + "ln_1.bias"])),
+                ln2=(f32(params[p + "ln_2.weight"]), f32(params[p + "ln_2.bias"])),
+                w_qkv=cdt(params[p + "attn.in_proj_weight"]), b_qkv=f32(params[p + "attn.in_proj_bias"]),
+                w_o=cdt(params[p + "attn.out_proj.weight"]), b_o=f32(params[p + "attn.out_proj.bias"]),
+                w_fc=cdt(params[p + "mlp.c_fc.weight"]), b_fc=f32(params[p + "mlp.c_fc.bias"]),
+                w_pr=cdt(params[p + "mlp.c_proj.weight"]), b_pr=f32(params[p + "mlp.c_proj.bias"]),
+            ))
+        self.adapted = text_adapter is not None
+        self.t_w = float(text_adapt_weight)
+        if self.adapted:
+            self.adapt_until = int(text_adapt_until)
+            self.w_adapt = [cdt(text_adapter[f"{i}.fc.0.weight"]) for i in range(self.adapt_until)]
+            self.w_out = cdt(text_adapter[f"{self.adapt_until}.fc.0.weight"])  # Linear + LeakyReLU
+        else:
+            self.adapt_until = 0
+            self.w_out = cdt(params["text_projection"].t())  # x @ P == x . (P^T)^T
+
+    @torch.no_grad()
+    def encode(self, tokens: torch.Tensor) -> torch.Tensor:
+        tokens = tokens.to(self.device, torch.int32).contiguous()
+        n, ctx = tokens.shape
+        if ctx != self.pos.shape[0]:
+            raise ValueError("token context length mismatch")
+        R, W = n * ctx, self.width
+        dev, cdt = self.device, self.dtype
+        e = lambda *s, dt=cdt: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+        X, H = e(R, W, dt=torch.float32), e(R, W)
+        qkv, att, fc, u = e(R, 3 * W), e(R, W), e(R, 4 * W), e(R, W, dt=torch.float32)
+        xb = e(R, W, dt=torch.bfloat16) if cdt == torch.bfloat16 else None
+        ops.text_embed_ln(tokens, self.tok_emb, self.pos, self.blocks[0]["ln1"], X, H)
+        nb = len(self.blocks)
+        for i, blk in enumerate(self.blocks):
+            ops.gemm(H, blk["w_qkv"], qkv, bias=blk["b_qkv"])
+            ops.attention(qkv, att, n, ctx, self.heads, causal=True)
+            ops.gemm(att, blk["w_o"], X, bias=blk["b_o"], residual=X)
+            ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], H)
+            ops.gemm(H, blk["w_fc"], fc, bias=blk["b_fc"], gelu=True)
+            adapt = i < self.adapt_until
+            ops.gemm(fc, blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=xb if (adapt and xb is not None) else None)
+            nxt = self.blocks[i + 1]["ln1"] if i + 1 < nb else None
+            if adapt:
+                ops.gemm(xb if xb is not None else X, self.w_adapt[i], u, leaky=True)
+                ops.block_tail(X, ctx, u=u, adapt_weight=self.t_w, ln=nxt, h=H if nxt else None)
+            elif nxt is not None:
+                ops.layernorm(X, nxt[0], nxt[1], H)
+        eot = e(n, W)
+        ops.eot_ln(X, tokens, self.ln_final, eot)
+        out = torch.empty(n, self.w_out.shape[0], device=dev, dtype=torch.float32)
+        ops.gemm(eot, self.w_out, out, leaky=self.adapted)
+        return out
+
+    @torch.no_grad()
+    def class_anchor(self, tok_normal: torch.Tensor, tok_abnormal: torch.Tensor) -> torch.Tensor:
+        """forward_utils.py:146-161 -> T [768, 2] (normal, abnormal)."""
+        T = torch.empty(self.w_out.shape[0], 2, device=self.device, dtype=torch.float32)
+        for col, tok in enumerate((tok_normal, tok_abnormal)):
+            ops.anchor_reduce(self.encode(tok), T, col)
+        return T

@@ -1,0 +1,253 @@
+"""Tensor-level wrappers over the C ABI (include/aaclip.h).
+
+torch is plumbing here: device memory, the current HIP stream, dtype tags.
+Every function validates shapes/dtypes on the host (a kernel is never launched
+on operands whose shapes disagree with what its grid assumes) and launches one
+HIP kernel on torch's current stream. There is no eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import BF16, F32, call
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dtag(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}; expected float32 or bfloat16") from None
+
+
+def torch_dtype(tag: int) -> torch.dtype:
+    return torch.float32 if tag == F32 else torch.bfloat16
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("aaclip ops need device (HIP) tensors; there is no CPU path")
+
+
+def _rowmajor(t: torch.Tensor, name: str):
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name} must be a 2-D tensor with unit column stride")
+
+
+# ------------------------------------------------------------------------ GEMM
+def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu=False, leaky=False,
+         residual=None, aux=None, row_group=0, row_group_out=0, row_offset=0) -> torch.Tensor:
+    """out = epilogue(a @ w.T) — a [M,K], w [N,K] (same dtype), out [M', N]."""
+    _dev(a, w, out, bias, residual, aux)
+    for t, n in ((a, "a"), (w, "w"), (out, "out")):
+        _rowmajor(t, n)
+    if a.dtype != w.dtype:
+        raise TypeError("gemm operands must share a dtype")
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K or out.shape[1] != N:
+        raise ValueError(f"gemm shape mismatch a{tuple(a.shape)} w{tuple(w.shape)} out{tuple(out.shape)}")
+    rows_out = M if row_group == 0 else ((M - 1) // row_group) * row_group_out + row_offset + (M - 1) % row_group + 1
+    if out.shape[0] < rows_out or (row_group and M % row_group):
+        raise ValueError("gemm output rows too small for the row remap")
+    epi = 0
+    if bias is not None:
+        if bias.dtype != torch.float32 or bias.numel() != N:
+            raise ValueError("bias must be fp32 [N]")
+        epi |= _lib.EPI_BIAS
+    if gelu:
+        epi |= _lib.EPI_GELU
+    if leaky:
+        epi |= _lib.EPI_LEAKY
+    ldr = 0
+    if residual is not None:
+        _rowmajor(residual, "residual")
+        if residual.dtype != torch.float32 or residual.shape[1] != N or residual.shape[0] < rows_out:
+            raise ValueError("residual must be fp32 [rows, N]")
+        epi |= _lib.EPI_RESID
+        ldr = residual.stride(0)
+    ldaux = 0
+    if aux is not None:
+        _rowmajor(aux, "aux")
+        if aux.dtype != torch.bfloat16 or aux.shape[1] != N or aux.shape[0] < rows_out:
+            raise ValueError("aux must be bf16 [rows, N]")
+        epi |= _lib.EPI_AUX_BF16
+        ldaux = aux.stride(0)
+    call("aaclip_gemm", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w), w.stride(0),
+         _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
+         row_group, row_group_out, row_offset, _stream())
+    return out
+
+
+# ------------------------------------------------------------------------ attention
+def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int,
+              causal: bool = False) -> torch.Tensor:
+    _dev(qkv, out)
+    hd = 64
+    if qkv.shape != (batch * seq, 3 * heads * hd) or out.shape != (batch * seq, heads * hd):
+        raise ValueError("attention shape mismatch")
+    if not (qkv.is_contiguous() and out.is_contiguous()) or qkv.dtype != out.dtype:
+        raise ValueError("attention tensors must be contiguous and share a dtype")
+    call("aaclip_attention", dtag(qkv), _ptr(qkv), _ptr(out), batch, seq, heads, hd, int(causal), _stream())
+    return out
+
+
+# ------------------------------------------------------------------------ rows
+def im2col(img: torch.Tensor, cols: torch.Tensor, patch: int) -> torch.Tensor:
+    _dev(img, cols)
+    B, C, S, S2 = img.shape
+    g = S // patch
+    if S != S2 or img.dtype != torch.float32 or not img.is_contiguous():
+        raise ValueError("image must be contiguous fp32 [B,C,S,S]")
+    if cols.shape[0] != B * g * g or not cols.is_contiguous():
+        raise ValueError("cols shape mismatch")
+    call("aaclip_im2col", dtag(cols), _ptr(img), _ptr(cols), B, C, S, patch, cols.shape[1], _stream())
+    return cols
+
+
+def embed_ln(x, cls, pos, ln_pre, ln1, h, batch, n_tok):
+    _dev(x, h)
+    width = x.shape[1]
+    if x.shape[0] != batch * n_tok or h.shape != x.shape or pos.shape != (n_tok, width):
+        raise ValueError("embed_ln shape mismatch")
+    call("aaclip_embed_ln", dtag(h), _ptr(x), _ptr(cls), _ptr(pos), _ptr(ln_pre[0]), _ptr(ln_pre[1]),
+         _ptr(ln1[0]), _ptr(ln1[1]), _ptr(h), batch, n_tok, width, _stream())
+
+
+def block_tail(x, n_tok, *, u=None, adapt_weight=0.0, ln=None, h=None, post=None, tap=None, out_dtype=None):
+    _dev(x, u, h, tap)
+    rows, width = x.shape
+    if u is not None and u.shape != x.shape:
+        raise ValueError("adapter output shape mismatch")
+    if h is not None and h.shape != x.shape:
+        raise ValueError("h shape mismatch")
+    if tap is not None and tap.shape != (rows // n_tok * (n_tok - 1), width):
+        raise ValueError("tap shape mismatch")
+    od = dtag(h) if h is not None else (dtag(tap) if tap is not None else F32)
+    if h is not None and tap is not None and h.dtype != tap.dtype:
+        raise ValueError("h and tap must share a dtype")
+    call("aaclip_block_tail", od, _ptr(x), _ptr(u), float(adapt_weight),
+         _ptr(ln[0]) if ln else None, _ptr(ln[1]) if ln else None, _ptr(h),
+         _ptr(post[0]) if post else None, _ptr(post[1]) if post else None, _ptr(tap),
+         rows, n_tok, width, _stream())
+
+
+def layernorm(x, w, b, y):
+    _dev(x, y)
+    _rowmajor(x, "x")
+    _rowmajor(y, "y")
+    if x.shape != y.shape or x.dtype != torch.float32:
+        raise ValueError("layernorm shape/dtype mismatch")
+    call("aaclip_layernorm", dtag(y), _ptr(x), x.stride(0), _ptr(w), _ptr(b), _ptr(y), y.stride(0),
+         x.shape[0], x.shape[1], _stream())
+    return y
+
+
+def text_embed_ln(tokens, tok_emb, pos, ln1, x, h):
+    _dev(tokens, x, h)
+    n, ctx = tokens.shape
+    if tokens.dtype != torch.int32 or not tokens.is_contiguous() or x.shape != (n * ctx, tok_emb.shape[1]):
+        raise ValueError("text_embed_ln shape mismatch")
+    call("aaclip_text_embed_ln", dtag(h), _ptr(tokens), _ptr(tok_emb), _ptr(pos), _ptr(ln1[0]), _ptr(ln1[1]),
+         _ptr(x), _ptr(h), n, ctx, x.shape[1], _stream())
+
+
+def eot_ln(x, tokens, ln, y):
+    _dev(x, tokens, y)
+    n, ctx = tokens.shape
+    if y.shape != (n, x.shape[1]) or x.shape[0] != n * ctx:
+        raise ValueError("eot_ln shape mismatch")
+    call("aaclip_eot_ln", dtag(y), _ptr(x), _ptr(tokens), _ptr(ln[0]), _ptr(ln[1]), _ptr(y), n, ctx,
+         x.shape[1], _stream())
+    return y
+
+
+def anchor_reduce(emb: torch.Tensor, T: torch.Tensor, col: int):
+    _dev(emb, T)
+    n, dim = emb.shape
+    if T.shape[0] != dim or emb.dtype != torch.float32 or not emb.is_contiguous():
+        raise ValueError("anchor_reduce shape mismatch")
+    call("aaclip_anchor_reduce", _ptr(emb), n, dim, _ptr(T), col, T.shape[1], _stream())
+
+
+def l2_normalize(x, y):
+    _dev(x, y)
+    _rowmajor(x, "x")
+    _rowmajor(y, "y")
+    if x.shape != y.shape:
+        raise ValueError("l2_normalize shape mismatch")
+    call("aaclip_l2_normalize", dtag(x), dtag(y), _ptr(x), x.stride(0), _ptr(y), y.stride(0),
+         x.shape[0], x.shape[1], _stream())
+    return y
+
+
+# ------------------------------------------------------------------------ anomaly map
+def _level_array(levels):
+    arr = (ctypes.c_void_p * len(levels))(*[t.data_ptr() for t in levels])
+    return arr
+
+
+def patch_scores(levels, T, out, *, normalize=True, mode=0):
+    _dev(*levels, T, out)
+    rows, C = levels[0].shape
+    for t in levels:
+        _rowmajor(t, "level")
+        if t.shape != (rows, C) or t.dtype != levels[0].dtype or t.stride(0) != levels[0].stride(0):
+            raise ValueError("levels must share shape, dtype and stride")
+    if T.shape != (C, 2) or T.dtype != torch.float32 or not T.is_contiguous():
+        raise ValueError("T must be contiguous fp32 [C, 2]")
+    need = rows if mode == 0 else 2 * rows
+    if out.numel() < need or out.dtype != torch.float32:
+        raise ValueError("patch_scores output too small")
+    arr = _level_array(levels)
+    call("aaclip_patch_scores", dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(T), rows, C,
+         int(normalize), mode, _ptr(out), _stream())
+    return out
+
+
+def blur_upsample(grid, out, *, ksize, sigma, softmax=False):
+    _dev(grid, out)
+    B, C, g, g2 = grid.shape
+    S = out.shape[-1]
+    if g != g2 or out.shape != (B, C, S, S) or not grid.is_contiguous() or not out.is_contiguous():
+        raise ValueError("blur_upsample shape mismatch")
+    call("aaclip_blur_upsample", _ptr(grid), _ptr(out), B, C, g, S, ksize, float(sigma), int(softmax), _stream())
+    return out
+
+
+def anomaly_map(levels, T, out, grid_ws, *, g, ksize, sigma, normalize=True):
+    _dev(*levels, T, out, grid_ws)
+    B, S, S2 = out.shape
+    rows, C = levels[0].shape
+    if rows != B * g * g or S != S2 or grid_ws.numel() < rows:
+        raise ValueError("anomaly_map shape mismatch")
+    for t in levels:
+        if t.shape != (rows, C) or t.stride(0) != levels[0].stride(0) or t.dtype != levels[0].dtype:
+            raise ValueError("levels must share shape, dtype and stride")
+    arr = _level_array(levels)
+    call("aaclip_anomaly_map", dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(T), B, g, C,
+         int(normalize), S, ksize, float(sigma), _ptr(grid_ws), _ptr(out), _stream())
+    return out
+
+
+def image_score(det_raw, batch, n_patch, partial, det=None, T=None, score=None, normalize=True):
+    _dev(det_raw, partial, det, T, score)
+    _rowmajor(det_raw, "det_raw")
+    rows, C = det_raw.shape
+    if rows != batch * n_patch or partial.numel() < batch * ((n_patch + 63) // 64) * C:
+        raise ValueError("image_score shape mismatch")
+    call("aaclip_image_score", dtag(det_raw), _ptr(det_raw), det_raw.stride(0), _ptr(T), batch, n_patch, C,
+         int(normalize), _ptr(partial), _ptr(det), _ptr(score), _stream())

@@ -1,0 +1,301 @@
+// Fused multi-head attention (flash-style, scores never leave the CU) for the
+// ViT-L/14 visual tower (seq 577 @336 px, 16 heads x 64) and the causal text
+// tower (seq 77, 12 heads x 64). Replaces torch F.multi_head_attention_forward
+// as called from nn.MultiheadAttention (reference model/transformer.py:200).
+//
+// bf16 kernel layout choices (gfx950, v_mfma_f32_16x16x32_bf16):
+//   * workgroup = 4 waves = 128 queries of one (image, head); wave = 2 x 16 queries
+//   * S^T = K . Q^T (keys on accumulator rows, the query on the lane): each lane
+//     owns one query's scores, so the softmax row reductions are in-register plus
+//     two cross-lane steps, and P^T leaves the accumulator already in the B-operand
+//     layout of the next MFMA — no LDS round trip for P.
+//   * O^T = V^T . P^T: the V^T operand comes from the row-major V tile through the
+//     gfx950 transposing LDS read ds_read_b64_tr_b16; the key order inside each
+//     32-key MFMA step is permuted consistently on both operands.
+//   * K/V tiles (64 keys) arrive by LDS-DMA (global_load_lds_dwordx4) into a
+//     double-buffered, XOR-swizzled LDS image; Q stays in registers.
+//   * online softmax in the log2 domain (v_exp_f32), fp32 statistics.
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+constexpr int HD_ = 64;      // head dim
+constexpr int KT = 64;       // keys per tile
+constexpr int QW = 32;       // queries per wave
+constexpr int NW = 4;        // waves per workgroup
+constexpr int QT = QW * NW;  // queries per workgroup
+
+__device__ __forceinline__ short4_t tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(p));
+}
+
+// byte offset of (row, 16-B chunk) in a swizzled [64][128 B] tile
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+__global__ __launch_bounds__(256) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
+                                                        uint16_t* __restrict__ out, int N, int H,
+                                                        int causal) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * KT * 128];  // [stage][K|V][64][128B]
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh % H;
+  const int HDt = H * HD_;
+  const int64_t ld = 3 * (int64_t)HDt;
+  const uint16_t* base = qkv + (size_t)b * N * ld + h * HD_;
+  const int q0 = blockIdx.x * QT + wid * QW;
+
+  // ---- Q fragments (B operand of K.Q^T): lane holds Q[q][ks*32 + 8g .. +7]
+  bf16x8_t qf[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = min(q0 + qb * 16 + c, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[qb][ks] = *(const bf16x8_t*)(base + (size_t)q * ld + ks * 32 + 8 * g);
+  }
+
+  // ---- DMA sources: wave w loads pieces i*4+w (8 rows each) of the K and V tiles
+  int row_of_piece[2];
+  const uint16_t* ksrc[2];
+  const uint16_t* vsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (i * NW + wid) * 8 + (lane >> 3);
+    row_of_piece[i] = r;
+    const int chunk = (lane & 7) ^ (r & 7);
+    ksrc[i] = base + HDt + chunk * 8;
+    vsrc[i] = base + 2 * HDt + chunk * 8;
+  }
+  auto stage = [&](int t, int buf) {
+    char* kb = smem + buf * (2 * KT * 128);
+    char* vb = kb + KT * 128;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int key = min(t * KT + row_of_piece[i], N - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(ksrc[i] + (size_t)key * ld),
+                                       LDS_PTR(kb + (i * NW + wid) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vsrc[i] + (size_t)key * ld),
+                                       LDS_PTR(vb + (i * NW + wid) * 1024), 16, 0, 0);
+    }
+  };
+
+  float4_t ot[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) ot[qb][db] = float4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY};
+  float l_run[2] = {0.f, 0.f};  // per-lane partial row sums (reduced over g at the end)
+  const float sl2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+
+  int ntiles = (N + KT - 1) / KT;
+  if (causal) {
+    const int last_q = min(blockIdx.x * QT + QT - 1, N - 1);
+    ntiles = min(ntiles, last_q / KT + 1);
+  }
+
+  stage(0, 0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) stage(t + 1, cur ^ 1);
+    const char* kt_lds = smem + cur * (2 * KT * 128);
+    const char* vt_lds = kt_lds + KT * 128;
+
+    // ---- S^T = K . Q^T : st[qb][kb][i] = S[q = qb*16+c][key = kb*16 + 4g + i]
+    float4_t st[2][4];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) st[qb][kb] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t kf = *(const bf16x8_t*)(kt_lds + swz(kb * 16 + c, ks * 4 + g));
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          st[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qb][ks], st[qb][kb], 0, 0, 0);
+      }
+    }
+
+    // ---- online softmax (log2 domain)
+    const int key0 = t * KT;
+    const bool tail = (key0 + KT > N) || causal;
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q = q0 + qb * 16 + c;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float s = st[qb][kb][i] * sl2;
+          if (tail) {
+            const int key = key0 + kb * 16 + 4 * g + i;
+            if (key >= N || (causal && key > q)) s = -INFINITY;
+          }
+          st[qb][kb][i] = s;
+          mx = fmaxf(mx, s);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run[qb], mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run[qb] - m_new);
+      m_run[qb] = m_new;
+      float ls = 0.f;
+      float p[4][4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          p[kb][i] = __builtin_amdgcn_exp2f(st[qb][kb][i] - m_new);
+          ls += p[kb][i];
+        }
+      l_run[qb] = l_run[qb] * alpha + ls;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) ot[qb][db] *= alpha;
+      // P^T as the B operand: k-step ks holds keys {32ks+4g+i} (j<4) and {32ks+16+4g+i} (j>=4)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = (__bf16)p[2 * ks][i];
+          v[4 + i] = (__bf16)p[2 * ks + 1][i];
+        }
+        pf[qb][ks] = v;
+      }
+    }
+
+    // ---- O^T += V^T . P^T ; V^T fragment via transposing LDS reads
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        // lane 4q+p of the 16-lane group addresses row (key) 32ks + [16] + 4g + q,
+        // columns d = db*16 + 4p .. +3
+        const int qq = c >> 2, pp = c & 3;
+        const int chunk = db * 2 + (pp >> 1);
+        const int r0 = ks * 32 + 4 * g + qq;
+        const short4_t lo = tr_read(vt_lds + swz(r0, chunk) + (pp & 1) * 8);
+        const short4_t hi = tr_read(vt_lds + swz(r0 + 16, chunk) + (pp & 1) * 8);
+        const short8_t vv = short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, vv);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          ot[qb][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb][ks], ot[qb][db], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: O[q][d = db*16 + 4g + i] = ot / l
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float l = l_run[qb];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    const int q = q0 + qb * 16 + c;
+    if (q < N) {
+      uint16_t* o = out + ((size_t)b * N + q) * HDt + h * HD_;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        uint2 r;
+        r.x = pack_bf16x2(ot[qb][db][0] * inv, ot[qb][db][1] * inv);
+        r.y = pack_bf16x2(ot[qb][db][2] * inv, ot[qb][db][3] * inv);
+        *(uint2*)(o + db * 16 + 4 * g) = r;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- fp32 (parity mode)
+// One thread per query; 64 queries per block; K/V tiles of 64 keys in LDS
+// (every lane reads the same K/V row -> LDS broadcast).
+__global__ __launch_bounds__(64) void attn_f32_kernel(const float* __restrict__ qkv,
+                                                      float* __restrict__ out, int N, int H,
+                                                      int causal) {
+  __shared__ float Ks[KT][HD_];
+  __shared__ float Vs[KT][HD_];
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh % H;
+  const int HDt = H * HD_;
+  const int64_t ld = 3 * (int64_t)HDt;
+  const float* base = qkv + (size_t)b * N * ld + h * HD_;
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  const int qc = min(q, N - 1);
+  float qv[HD_], o[HD_];
+#pragma unroll
+  for (int d = 0; d < HD_; ++d) {
+    qv[d] = base[(size_t)qc * ld + d] * 0.125f;
+    o[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  int ntiles = (N + KT - 1) / KT;
+  if (causal) ntiles = min(ntiles, min(blockIdx.x * 64 + 63, N - 1) / KT + 1);
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < KT * HD_; i += 64) {
+      const int r = i / HD_, d = i % HD_;
+      const int key = min(t * KT + r, N - 1);
+      Ks[r][d] = base[(size_t)key * ld + HDt + d];
+      Vs[r][d] = base[(size_t)key * ld + 2 * HDt + d];
+    }
+    __syncthreads();
+    float s[KT];
+    float mx = -INFINITY;
+#pragma unroll 4
+    for (int j = 0; j < KT; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < HD_; ++d) acc = fmaf(qv[d], Ks[j][d], acc);
+      const int key = t * KT + j;
+      if (key >= N || (causal && key > qc)) acc = -INFINITY;
+      s[j] = acc;
+      mx = fmaxf(mx, acc);
+    }
+    const float m_new = fmaxf(m, mx);
+    const float alpha = expf(m - m_new);
+    l *= alpha;
+#pragma unroll
+    for (int d = 0; d < HD_; ++d) o[d] *= alpha;
+#pragma unroll 4
+    for (int j = 0; j < KT; ++j) {
+      const float p = expf(s[j] - m_new);
+      l += p;
+#pragma unroll
+      for (int d = 0; d < HD_; ++d) o[d] = fmaf(p, Vs[j][d], o[d]);
+    }
+    m = m_new;
+  }
+  if (q < N) {
+    float* op = out + ((size_t)b * N + q) * HDt + h * HD_;
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int d = 0; d < HD_; ++d) op[d] = o[d] * inv;
+  }
+}
+
+}  // namespace
+
+extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
+                                int heads, int head_dim, int causal, void* stream) {
+  AACLIP_REQUIRE(dtype == AACLIP_F32 || dtype == AACLIP_BF16);
+  AACLIP_REQUIRE(qkv && out && batch > 0 && seq > 0 && heads > 0 && head_dim == HD_);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == AACLIP_BF16) {
+    dim3 grid(ceil_div(seq, QT), batch * heads);
+    attn_bf16_kernel<<<grid, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, seq, heads, causal);
+  } else {
+    dim3 grid(ceil_div(seq, 64), batch * heads);
+    attn_f32_kernel<<<grid, 64, 0, s>>>((const float*)qkv, (float*)out, seq, heads, causal);
+  }
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}

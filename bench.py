@@ -1,0 +1,260 @@
+"""AA-CLIP anomaly-map inference benchmark on MI355X (BASELINE.json metric:
+images/sec at 336x336, ViT-L/14, + pixel-map parity vs the CPU reference).
+
+One step = one batch of 32 synthetic 336x336 images per GPU through the full
+hot path, inputs already resident in HBM: ViT-L/14-336 visual tower with the 6
+residual adapters, 4 level taps + seg/det projections, fused anomaly map
+(Industrial blur) and image scores; for N > 1 the per-image scores are
+all-gathered over RCCL (the path's only exchange). Weights: random-init
+synthetic (no checkpoint in the image), bf16 compute.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with a
+`roofline` object for the dominant kernel (bf16 GEMM, MFMA-bound), a
+`roofline_map` object for the anomaly-map stream kernel (HBM-bound) and a
+`cpu_baseline` measured with the numpy oracle on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "aa-clip_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from aaclip import ops  # noqa: E402
+from aaclip.engine import HEADS, LAYERS, WIDTH, VisualEngine  # noqa: E402
+
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0      # HBM3E spec peak
+
+
+def synthetic_visual_weights(dev, seed=111, n_levels=4, adapt_until=6):
+    """Random-init ViT-L/14-336 + adapters, generated on device (reference key names)."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    r = lambda *s, std=1.0: torch.randn(*s, device=dev, generator=g) * std  # noqa: E731
+    W = WIDTH
+    vp = {
+        "visual.conv1.weight": r(W, 3, 14, 14, std=588 ** -0.5),
+        "visual.class_embedding": r(W, std=W ** -0.5),
+        "visual.positional_embedding": r(577, W, std=W ** -0.5),
+        "visual.ln_pre.weight": 1 + r(W, std=0.1), "visual.ln_pre.bias": r(W, std=0.05),
+        "visual.ln_post.weight": 1 + r(W, std=0.1), "visual.ln_post.bias": r(W, std=0.05),
+    }
+    for i in range(LAYERS):
+        p = f"visual.transformer.resblocks.{i}."
+        vp.update({
+            p + "ln_1.weight": 1 + r(W, std=0.1), p + "ln_1.bias": r(W, std=0.05),
+            p + "ln_2.weight": 1 + r(W, std=0.1), p + "ln_2.bias": r(W, std=0.05),
+            p + "attn.in_proj_weight": r(3 * W, W, std=W ** -0.5), p + "attn.in_proj_bias": r(3 * W, std=0.02),
+            p + "attn.out_proj.weight": r(W, W, std=W ** -0.5), p + "attn.out_proj.bias": r(W, std=0.02),
+            p + "mlp.c_fc.weight": r(4 * W, W, std=(2 * W) ** -0.5), p + "mlp.c_fc.bias": r(4 * W, std=0.02),
+            p + "mlp.c_proj.weight": r(W, 4 * W, std=(4 * W) ** -0.5), p + "mlp.c_proj.bias": r(W, std=0.02),
+        })
+    ad = {f"layer_adapters.{i}.fc.0.weight": r(W, W, std=0.03) for i in range(adapt_until)}
+    ad.update({f"seg_proj.{i}.fc.weight": r(768, W, std=0.03) for i in range(n_levels)})
+    ad["det_proj.fc.weight"] = r(768, W, std=0.03)
+    return vp, ad
+
+
+def flops_per_image(n_tok=577, levels=4, adapt=6):
+    """Algorithmic FLOPs: GEMMs 2MKN, attention 4 N^2 d per layer."""
+    P = n_tok - 1
+    W = WIDTH
+    blocks = LAYERS * (2 * n_tok * W * 3 * W + 4 * n_tok * n_tok * W + 2 * n_tok * W * W + 2 * 2 * n_tok * W * 4 * W)
+    return blocks + 2 * P * 588 * W + adapt * 2 * n_tok * W * W + levels * 2 * P * W * 768 + 2 * P * W * 768
+
+
+def time_launches(fn, reps, stream):
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    fn()
+    start.record(stream)
+    for _ in range(reps):
+        fn()
+    end.record(stream)
+    end.synchronize()
+    return start.elapsed_time(end) / reps  # ms per launch
+
+
+def roofline_gemm(eng, ws, reps=20):
+    """Dominant kernel = bf16 MFMA GEMM <256x256> (QKV and c_fc launches).
+    Average HIP-event launch duration over the two shapes it runs at."""
+    s = torch.cuda.current_stream()
+    blk = eng.blocks[0]
+    R = ws["x"].shape[0]
+    t_qkv = time_launches(lambda: ops.gemm(ws["h"], blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"]), reps, s)
+    t_fc = time_launches(lambda: ops.gemm(ws["h"], blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True), reps, s)
+    f_qkv = 2.0 * R * WIDTH * 3 * WIDTH
+    f_fc = 2.0 * R * WIDTH * 4 * WIDTH
+    t_avg = (t_qkv + t_fc) / 2
+    achieved = (f_qkv + f_fc) / 2 / (t_avg * 1e-3) / 1e12
+    # attention + MLP block GEMMs incl. the 256x128 launches (out-proj, c_proj)
+    t_o = time_launches(lambda: ops.gemm(ws["attn"], blk["w_o"], ws["u"], bias=blk["b_o"]), reps, s)
+    t_pr = time_launches(lambda: ops.gemm(ws["fc"], blk["w_pr"], ws["u"], bias=blk["b_pr"]), reps, s)
+    t_at = time_launches(lambda: ops.attention(ws["qkv"], ws["attn"], R // ws["n_tok"], ws["n_tok"], HEADS), reps, s)
+    n = ws["n_tok"]
+    B = R // n
+    f_at = 4.0 * B * n * n * WIDTH
+    block_flops = f_qkv + f_fc + 2.0 * R * WIDTH * WIDTH + 2.0 * R * 4 * WIDTH * WIDTH + f_at
+    block_ms = t_qkv + t_fc + t_o + t_pr + t_at
+    return {
+        "kernel": "gemm_bf16_kernel<256,256,2,4> (QKV + c_fc launches)",
+        "bound": "mfma", "unit": "TFLOP/s", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS,
+        "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+        "avg_launch_us": round(t_avg * 1e3, 2),
+        "flops_per_launch": (f_qkv + f_fc) / 2,
+        "attn_mlp_block": {"tflops": round(block_flops / (block_ms * 1e-3) / 1e12, 1),
+                           "frac": round(block_flops / (block_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4),
+                           "ms": {"qkv": round(t_qkv, 4), "attn": round(t_at, 4), "out": round(t_o, 4),
+                                  "fc": round(t_fc, 4), "proj": round(t_pr, 4)},
+                           "attention_tflops": round(f_at / (t_at * 1e-3) / 1e12, 1)},
+    }
+
+
+def roofline_map(eng, ws, T, reps=50):
+    """Anomaly-map stream kernel (patch_scores): algorithmic bytes = L*P*768*2 (bf16
+    features) + 768*2*4 (anchors) + P*4 (score grid) per image."""
+    s = torch.cuda.current_stream()
+    L = ws["segbuf"].shape[1] // 768 - 1
+    seg = [ws["segbuf"][:, j * 768:(j + 1) * 768] for j in range(L)]
+    rows = seg[0].shape[0]
+    t_ps = time_launches(lambda: ops.patch_scores(seg, T, ws["grid"]), reps, s)
+    nbytes = len(seg) * rows * 768 * 2 + 768 * 2 * 4 + rows * 4
+    B = rows // ws["P"]
+    S = ws["map"].shape[-1]
+    g = ws["g"]
+    t_bu = time_launches(lambda: ops.blur_upsample(ws["grid"].view(B, 1, g, g), ws["map"].view(B, 1, S, S),
+                                                   ksize=7, sigma=1.0), reps, s)
+    gbs = nbytes / (t_ps * 1e-3) / 1e9
+    return {"kernel": "patch_scores_kernel", "bound": "hbm", "unit": "GB/s", "achieved": round(gbs, 1),
+            "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "avg_launch_us": round(t_ps * 1e3, 2), "bytes_per_launch": nbytes,
+            "blur_upsample_us": round(t_bu * 1e3, 2),
+            "blur_upsample_GBs": round(B * S * S * 4 / (t_bu * 1e-3) / 1e9, 1)}
+
+
+def cpu_baseline(n_images: int):
+    """The numpy oracle (fp32 restatement of the reference, pinned to its golden
+    vectors) on this host's cores: forward + 4-level map + image score."""
+    import numpy as np
+
+    from oracle import aaclip_np as R
+    from oracle import synth
+    sd = synth.clip_state_dict(111)
+    ia, _ = synth.adapter_state_dicts(111)
+    x = synth.images(111, n_images, 336)
+    T = np.linalg.qr(np.random.default_rng(0).standard_normal((768, 2)))[0].astype(np.float32)
+    R.visual_forward(sd, ia, x[:1])  # warm-up (BLAS threads, page-in)
+    t0 = time.perf_counter()
+    for i in range(n_images):
+        seg, det = R.visual_forward(sd, ia, x[i:i + 1])
+        R.anomaly_map(seg, T, 336, "Industrial")
+        R.image_score(det, T)
+    dt = time.perf_counter() - t0
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": round(n_images / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"{n_images} synthetic 336px images, bs=1, fp32 numpy oracle (oracle/aaclip_np.py), "
+                      f"{dt:.1f} s", "threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--img-size", type=int, default=336)
+    ap.add_argument("--cpu-images", type=int, default=2, help="images for the CPU baseline (0 = skip)")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    vp, ad = synthetic_visual_weights(dev)
+    eng = VisualEngine(vp, ad, dtype=torch.bfloat16)
+    del vp
+    B, S = args.batch, args.img_size
+    g = torch.Generator(device=dev).manual_seed(111 + rank)
+    x = torch.randn(B, 3, S, S, device=dev, generator=g)
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
+    gathered = torch.empty(world * B, device=dev) if world > 1 else None
+
+    def step():
+        maps, score = eng.predict(x, T, "Industrial")
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, score)
+        return maps
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    images = B * world * args.steps
+    ms_per_step = elapsed / args.steps * 1e3
+    ws = eng._workspace(B, S)
+    line = {
+        "metric": "images/sec (336x336, ViT-L/14) + pixel-AUROC parity vs CPU ref",
+        "value": round(images / elapsed, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (N(0,1) images on device, random-init ViT-L/14-336 + adapters)",
+        "config": {"workload": "C2: AA-CLIP anomaly-map inference, ViT-L/14-336, bf16, 4 levels, 2 anchors, "
+                               "Industrial blur, per-GPU batch of images",
+                   "global_batch": B * world, "img_size": S, "per_gpu_batch": B,
+                   "parallelism": f"image-sharded dp{world} (+RCCL all-gather of image scores)",
+                   "gflop_per_image": round(flops_per_image((S // 14) ** 2 + 1) / 1e9, 2)},
+    }
+    line["tflops_whole_path"] = round(flops_per_image((S // 14) ** 2 + 1) * images / elapsed / 1e12, 1)
+    if rank == 0 and not args.no_roofline:
+        line["roofline"] = roofline_gemm(eng, ws)
+        line["roofline_map"] = roofline_map(eng, ws, T)
+    if rank == 0 and world == 1 and args.cpu_images > 0:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_images)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

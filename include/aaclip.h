@@ -1,0 +1,191 @@
+/*
+ * aaclip.h — C ABI of libaaclip_hip.so, the MI355X (gfx950) kernels behind
+ * AA-CLIP's anomaly-map inference path.
+ *
+ * Conventions (every entry point):
+ *   - extern "C", stateless, re-entrant; returns 0 (AACLIP_OK) or an error
+ *     code (AACLIP_ERR_ARG for a rejected argument, AACLIP_ERR_LAUNCH + hipError_t
+ *     when the launch itself failed).
+ *   - All tensor arguments are caller-owned DEVICE pointers (the caller's
+ *     allocator owns them; nothing here allocates, frees or synchronises, so every
+ *     call can be captured into a hipGraph). Row-major, leading dimensions in
+ *     ELEMENTS. `stream` is a hipStream_t passed as void*.
+ *   - dtype enums: AACLIP_F32 = 0, AACLIP_BF16 = 1. bf16 is stored as uint16.
+ *
+ * The reference (wei-paul/AA-CLIP) has no native code: each entry point below
+ * replaces the PyTorch/kornia call sites cited next to it
+ * (paths relative to the reference root). The binding a maintainer adds on the
+ * reference side is the ctypes stub shown in INTEGRATION.md.
+ */
+#ifndef AACLIP_H_
+#define AACLIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AACLIP_OK 0
+#define AACLIP_ERR_ARG 1
+#define AACLIP_ERR_LAUNCH 1000
+
+#define AACLIP_F32 0
+#define AACLIP_BF16 1
+
+/* GEMM epilogue flags (applied in this order) */
+#define AACLIP_EPI_BIAS 1      /* + bias[n] (fp32)                          */
+#define AACLIP_EPI_GELU 2      /* exact erf GELU (nn.GELU)                  */
+#define AACLIP_EPI_LEAKY 4     /* LeakyReLU(0.01) (nn.LeakyReLU)            */
+#define AACLIP_EPI_RESID 8     /* + residual[row, n] (fp32; may alias C)    */
+#define AACLIP_EPI_AUX_BF16 16 /* also store a bf16 copy of the result      */
+
+/* ABI version (bumped on any signature change) and the compiled target. */
+int aaclip_abi_version(void);
+const char* aaclip_arch(void);
+
+/*
+ * C[M,N] = epilogue(A[M,K] . W[N,K]^T)        (nn.Linear / conv-as-GEMM)
+ * Replaces: every addmm/mm of the path — MHA in_proj / out_proj
+ * (model/transformer.py:200 via torch F.multi_head_attention_forward), MLP
+ * c_fc + GELU and c_proj (transformer.py:211-219, :256-257), conv1 as GEMM
+ * (transformer.py:359-365), adapter Linear+LeakyReLU (model/adapter_modules.py:6-26,
+ * model/adapter.py:93), seg_proj/det_proj (adapter.py:107-110), text projection
+ * (adapter.py:140, model/model.py:200).
+ * in_dtype: A and W (bf16 -> bf16 MFMA, f32 -> f32 MFMA). out_dtype: C.
+ * K % 64 == 0 (bf16) / K % 16 == 0 (f32); lda, ldw multiples of 8.
+ * Output row remap when row_group > 0:
+ *   out_row = (m / row_group) * row_group_out + row_offset + (m % row_group)
+ * (used to write patch embeddings after each image's CLS slot). The same
+ * remapped row indexes `residual` and `aux`.
+ */
+int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K,
+                const void* A, int64_t lda, const void* W, int64_t ldw,
+                void* C, int64_t ldc, int epilogue, const float* bias,
+                const float* residual, int64_t ldr, void* aux, int64_t ldaux,
+                int row_group, int row_group_out, int row_offset, void* stream);
+
+/*
+ * Multi-head attention core, softmax(q k^T / sqrt(d)) v per head, flash-style
+ * (scores never materialised). qkv: [batch*seq, 3*heads*head_dim] packed
+ * [q|k|v] exactly as nn.MultiheadAttention's in_proj output; out:
+ * [batch*seq, heads*head_dim] (heads merged, ready for out_proj).
+ * causal != 0 adds the text tower's -inf upper triangle
+ * (transformer.py:629-635). head_dim must be 64.
+ * Replaces: torch F.multi_head_attention_forward's q-scale/bmm/softmax/bmm
+ * (transformer.py:200, need_weights=True branch; the averaged weights are
+ * discarded by the caller, model/adapter.py:91 — never computed here).
+ */
+int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
+                     int heads, int head_dim, int causal, void* stream);
+
+/*
+ * Patchify for conv1-as-GEMM: img [batch, channels, S, S] fp32 ->
+ * cols [batch*(S/patch)^2, k_padded], column k = c*patch*patch + kh*patch + kw
+ * (conv weight flattening order), zero for k >= channels*patch^2.
+ * Replaces: the im2col inside conv1 (model/adapter.py:68).
+ */
+int aaclip_im2col(int out_dtype, const float* img, void* cols, int batch, int channels,
+                  int img_size, int patch, int k_padded, void* stream);
+
+/*
+ * Visual token assembly + ln_pre + block-0 ln_1, one row per token:
+ *   e = (t == 0 ? cls : x[row]) + pos[t];  x[row] = LN_pre(e);  h[row] = LN_1(x[row])
+ * x: [batch*n_tok, width] fp32, rows t>=1 already hold conv1 patch embeddings.
+ * Replaces: model/adapter.py:72-85 + the first ln_1 (transformer.py:254).
+ */
+int aaclip_embed_ln(int out_dtype, float* x, const float* cls, const float* pos,
+                    const float* ln_pre_w, const float* ln_pre_b, const float* ln1_w,
+                    const float* ln1_b, void* h, int batch, int n_tok, int width, void* stream);
+
+/*
+ * Row epilogue after a residual block (all optional stages, one pass):
+ *   if u:   x = w*(u*||x||/||u||) + (1-w)*x              (adapter blend)
+ *   if h:   h = LN(x; ln_w, ln_b)                         (next block's ln_1)
+ *   if tap: tap[b*(n_tok-1)+t-1] = LN(x; post_w, post_b)  for t >= 1 (level tap + ln_post)
+ * x: [rows, width] fp32, rows = batch*n_tok.
+ * Replaces: model/adapter.py:92-101 (image) / :129-136 (text), the ln_1 of
+ * transformer.py:254, and ln_post of level taps (adapter.py:100-105).
+ */
+int aaclip_block_tail(int out_dtype, float* x, const float* u, float adapt_weight,
+                      const float* ln_w, const float* ln_b, void* h, const float* post_w,
+                      const float* post_b, void* tap, int rows, int n_tok, int width,
+                      void* stream);
+
+/* y = LN(x) rows (F.layer_norm, eps 1e-5, biased variance; transformer.py:37-43). */
+int aaclip_layernorm(int out_dtype, const float* x, int64_t ldx, const float* w,
+                     const float* b, void* y, int64_t ldy, int rows, int width, void* stream);
+
+/*
+ * Text embedding: x[s*ctx+t] = tok_emb[tokens[s,t]] + pos[t]; h = LN_1(x).
+ * Replaces: model/adapter.py:118-123 / model/model.py:192-194 + first ln_1.
+ */
+int aaclip_text_embed_ln(int out_dtype, const int32_t* tokens, const float* tok_emb,
+                         const float* pos, const float* ln1_w, const float* ln1_b, float* x,
+                         void* h, int n_seq, int ctx, int width, void* stream);
+
+/*
+ * EOT gather + ln_final: y[s] = LN(x[s*ctx + argmax_t tokens[s,t]]).
+ * Replaces: model/adapter.py:138-140 / model/model.py:199-200.
+ */
+int aaclip_eot_ln(int out_dtype, const float* x, const int32_t* tokens, const float* w,
+                  const float* b, void* y, int n_seq, int ctx, int width, void* stream);
+
+/*
+ * Prompt-ensemble anchor: T[:, col] = normalize(mean_s normalize(emb[s])).
+ * T: [dim, ncols] fp32. Replaces: forward_utils.py:155-159.
+ */
+int aaclip_anchor_reduce(const float* emb, int n, int dim, float* T, int col, int ncols,
+                         void* stream);
+
+/* y = x / max(||x||, 1e-12) per row (F.normalize, model/adapter.py:109). */
+int aaclip_l2_normalize(int in_dtype, int out_dtype, const void* x, int64_t ldx, void* y,
+                        int64_t ldy, int rows, int width, void* stream);
+
+/*
+ * Patch x anchor similarity for n_levels feature tensors (levels: HOST array
+ * of n_levels device pointers, each [rows, channels], row stride ld):
+ *   f_hat = normalize ? f/max(||f||,1e-12) : f;  A_c = 100 * f_hat . T[:, c]
+ *   mode 0 (test): out[row] = sum_l (A_1 + 1 - A_0) / 2
+ *   mode 1 (train, n_levels == 1): out[row*2 + c] = A_c
+ * T: [channels, 2] fp32. Replaces: forward_utils.py:199-207 (+ the level sum of
+ * test.py:93, moved before the blur/upsample: both are linear).
+ */
+int aaclip_patch_scores(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
+                        const float* T, int rows, int channels, int normalize, int mode,
+                        float* out, void* stream);
+
+/*
+ * Gaussian blur (kornia 0.6.9 gaussian_blur2d, reflect border, separable;
+ * skipped when ksize == 0) then bilinear upsample with align_corners=True
+ * (F.interpolate), optional softmax over the channel dim (train branch).
+ * grid: [batch, channels, g, g] fp32 -> out [batch, channels, S, S] fp32.
+ * Replaces: forward_utils.py:208-215.
+ */
+int aaclip_blur_upsample(const float* grid, float* out, int batch, int channels, int g,
+                         int out_size, int ksize, float sigma, int softmax, void* stream);
+
+/*
+ * Full test-branch anomaly map for one batch: patch_scores (mode 0) into the
+ * caller's workspace grid_ws [batch*g*g] fp32, then blur + upsample into
+ * out [batch, S, S]. Replaces: test.py:86-93 + forward_utils.py:196-213.
+ */
+int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
+                       const float* T, int batch, int g, int channels, int normalize,
+                       int out_size, int ksize, float sigma, float* grid_ws, float* out,
+                       void* stream);
+
+/*
+ * Image-level score: det[b] = mean_p normalize(det_raw[b*n_patch+p]) and
+ * score[b] = (det[b] . T[:,1] + 1) / 2. partial: workspace
+ * [batch, ceil(n_patch/64), channels] fp32 (fixed-order reduction, deterministic).
+ * Replaces: model/adapter.py:110-111 + test.py:83-84.
+ */
+int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld, const float* T,
+                       int batch, int n_patch, int channels, int normalize, float* partial,
+                       float* det, float* score, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AACLIP_H_ */

@@ -1,0 +1,240 @@
+"""Per-kernel parity on the MI355X: each HIP kernel vs a plain fp32 reference
+(torch fp32 / float64 on the host for the floating-point kernels, the numpy
+oracle for the row ops, the reference's own golden vectors where they exist).
+All calls go through the C ABI (libaaclip_hip.so via aaclip.ops)."""
+import numpy as np
+import pytest
+import torch
+
+from aaclip import ops
+from oracle import aaclip_np as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+# ----------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (1154, 1024, 4096), (37, 768, 1024), (513, 1536, 1024),
+                                   (600, 4096, 1024), (256 * 9, 2304, 768)])
+def test_gemm_bf16_plain(dev, M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to(dev)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)
+    ab, wb = a.bfloat16(), w.bfloat16()
+    out = torch.empty(M, N, device=dev, dtype=torch.float32)
+    ops.gemm(ab, wb, out)
+    ref = ab.double() @ wb.double().T
+    err = (out.double() - ref).abs().max().item()
+    assert err < 1e-3 * ref.abs().max().item() + 1e-4, err
+
+
+def test_gemm_bf16_asymmetric_identity(dev):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    M = N = K = 256
+    a = torch.eye(M, K, device=dev, dtype=torch.bfloat16)
+    w = (torch.arange(N * K, device=dev, dtype=torch.float32).reshape(N, K) % 97).bfloat16()
+    out = torch.empty(M, N, device=dev)
+    ops.gemm(a, w, out)
+    torch.testing.assert_close(out, w.float().T, atol=0, rtol=0)
+
+
+def test_gemm_epilogues_bf16(dev):
+    torch.manual_seed(0)
+    M, N, K = 700, 1024, 1024
+    a = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.03).bfloat16()
+    bias = torch.randn(N, device=dev)
+    base = a.double() @ w.double().T + bias.double()
+    # bias + gelu -> bf16
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, w, out, bias=bias, gelu=True)
+    ref = torch.nn.functional.gelu(base)
+    assert (out.double() - ref).abs().max().item() < 2e-2
+    # leaky -> fp32
+    out32 = torch.empty(M, N, device=dev)
+    ops.gemm(a, w, out32, leaky=True)
+    ref = torch.nn.functional.leaky_relu(a.double() @ w.double().T, 0.01)
+    assert (out32.double() - ref).abs().max().item() < 1e-3
+    # bias + residual in place + aux bf16 copy
+    x = torch.randn(M, N, device=dev)
+    x0 = x.clone()
+    aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, w, x, bias=bias, residual=x, aux=aux)
+    ref = base + x0.double()
+    assert (x.double() - ref).abs().max().item() < 1e-3
+    assert torch.equal(aux, x.bfloat16())
+
+
+def test_gemm_row_remap(dev):
+    """Patch-embedding rows land after each image's CLS slot (row_group)."""
+    B, P, K, N = 3, 576, 640, 1024
+    a = torch.randn(B * P, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.04).bfloat16()
+    x = torch.full((B * (P + 1), N), 7.0, device=dev)
+    ops.gemm(a, w, x, row_group=P, row_group_out=P + 1, row_offset=1)
+    ref = (a.double() @ w.double().T).view(B, P, N)
+    xv = x.view(B, P + 1, N)
+    assert torch.all(xv[:, 0] == 7.0)
+    assert (xv[:, 1:].double() - ref).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(577 * 2, 3072, 1024), (77 * 6, 768, 3072), (33, 64, 16)])
+def test_gemm_f32(dev, M, N, K):
+    a = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) * K ** -0.5
+    b = torch.randn(N, device=dev)
+    out = torch.empty(M, N, device=dev)
+    ops.gemm(a, w, out, bias=b)
+    ref = a.double() @ w.double().T + b.double()
+    assert (out.double() - ref).abs().max().item() < 2e-5 * (K ** 0.5)
+
+
+# ----------------------------------------------------------------------------- attention
+def _attn_ref(qkv, B, N, H, causal):
+    D = H * 64
+    q, k, v = qkv.double().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q * 0.125) @ k.transpose(-1, -2)
+    if causal:
+        s = s + torch.triu(torch.full((N, N), float("-inf"), device=s.device, dtype=s.dtype), 1)
+    o = torch.softmax(s, -1) @ v
+    return o.permute(0, 2, 1, 3).reshape(B * N, D)
+
+
+@pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (1, 1025, 16, False),
+                                          (2, 5, 2, False), (4, 130, 4, True)])
+def test_attention_bf16(dev, B, N, H, causal):
+    torch.manual_seed(B * N + H)
+    qkv = (torch.randn(B * N, 3 * H * 64, device=dev) * 1.5).bfloat16()
+    out = torch.empty(B * N, H * 64, device=dev, dtype=torch.bfloat16)
+    ops.attention(qkv, out, B, N, H, causal=causal)
+    ref = _attn_ref(qkv, B, N, H, causal)
+    err = (out.double() - ref).abs().max().item()
+    assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (3, 77, 12, True)])
+def test_attention_f32(dev, B, N, H, causal):
+    torch.manual_seed(1)
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev)
+    out = torch.empty(B * N, H * 64, device=dev)
+    ops.attention(qkv, out, B, N, H, causal=causal)
+    ref = _attn_ref(qkv, B, N, H, causal)
+    assert (out.double() - ref).abs().max().item() < 1e-5
+
+
+def test_attention_spiky_rows(dev):
+    """Force the online-softmax rescale: one key spikes late in the sequence."""
+    B, N, H = 1, 577, 2
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev) * 0.1
+    qkv[:, :64] = 1.0
+    qkv[500, H * 64:H * 64 + 64] = 3.0  # key 500, head 0: huge logit for every query
+    for dt in (torch.bfloat16, torch.float32):
+        x = qkv.to(dt)
+        out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
+        ops.attention(x, out, B, N, H)
+        ref = _attn_ref(x, B, N, H, False)
+        assert (out.double() - ref).abs().max().item() < (2e-2 if dt == torch.bfloat16 else 1e-5)
+
+
+# ----------------------------------------------------------------------------- rows
+def test_layernorm_vs_reference(dev, golden):
+    o = golden["ops"]
+    x = torch.from_numpy(o["ln_x"]).to(dev)
+    from oracle import synth
+    sd = synth.clip_state_dict(111)
+    w = torch.from_numpy(sd["visual.ln_pre.weight"]).to(dev)
+    b = torch.from_numpy(sd["visual.ln_pre.bias"]).to(dev)
+    y = torch.empty_like(x)
+    ops.layernorm(x, w, b, y)
+    np.testing.assert_allclose(y.cpu().numpy(), o["ln_y"], atol=2e-5, rtol=1e-5)
+
+
+def test_block_tail_and_embed(dev):
+    rng = np.random.default_rng(0)
+    B, n_tok, D = 2, 577, 1024
+    x = rng.standard_normal((B * n_tok, D), dtype=np.float32)
+    u = rng.standard_normal((B * n_tok, D), dtype=np.float32)
+    lw, lb = (1 + 0.1 * rng.standard_normal(D)).astype(np.float32), (0.1 * rng.standard_normal(D)).astype(np.float32)
+    pw, pb = (1 + 0.1 * rng.standard_normal(D)).astype(np.float32), (0.1 * rng.standard_normal(D)).astype(np.float32)
+    X = torch.from_numpy(x).to(dev)
+    H = torch.empty(B * n_tok, D, device=dev)
+    tap = torch.empty(B * (n_tok - 1), D, device=dev)
+    t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    ops.block_tail(X, n_tok, u=t(u), adapt_weight=0.1, ln=(t(lw), t(lb)), h=H, post=(t(pw), t(pb)), tap=tap)
+    xn = np.linalg.norm(x, axis=-1, keepdims=True)
+    un = np.linalg.norm(u, axis=-1, keepdims=True)
+    xr = 0.1 * (u * xn / un) + 0.9 * x
+    np.testing.assert_allclose(X.cpu().numpy(), xr, atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(H.cpu().numpy(), R.layer_norm(xr, lw, lb), atol=1e-4, rtol=1e-4)
+    tr = R.layer_norm(xr.reshape(B, n_tok, D)[:, 1:], pw, pb).reshape(-1, D)
+    np.testing.assert_allclose(tap.cpu().numpy(), tr, atol=1e-4, rtol=1e-4)
+
+
+# ----------------------------------------------------------------------------- anomaly map
+@pytest.mark.parametrize("dom", ["Industrial", "Medical"])
+def test_similarity_map_golden(dev, golden, dom):
+    """Reference calculate_similarity_map (test branch) on a 8x8 grid -> 40x40."""
+    o = golden["ops"]
+    f = torch.from_numpy(o["sim_f"]).to(dev)  # [2, 64, 32] unit rows, C=32
+    T = torch.from_numpy(o["sim_T"]).to(dev)
+    # the kernel needs C = 768: embed the 32 channels in 768 zero-padded ones (exact)
+    fp = torch.zeros(2 * 64, 768, device=dev)
+    fp[:, :32] = f.reshape(-1, 32)
+    Tp = torch.zeros(768, 2, device=dev)
+    Tp[:32] = T
+    grid = torch.empty(2 * 64, device=dev)
+    ops.patch_scores([fp], Tp, grid)
+    out = torch.empty(2, 1, 40, 40, device=dev)
+    k, s = (7, 1.0) if dom == "Industrial" else (9, 1.5)
+    ops.blur_upsample(grid.view(2, 1, 8, 8), out, ksize=k, sigma=s)
+    np.testing.assert_allclose(out.cpu().numpy(), o[f"sim_test_{dom}"], atol=1e-5, rtol=1e-5)
+
+
+def test_similarity_map_train_golden(dev, golden):
+    o = golden["ops"]
+    f = torch.from_numpy(o["sim_f"]).to(dev)
+    T = torch.from_numpy(o["sim_T"]).to(dev)
+    fp = torch.zeros(2 * 64, 768, device=dev)
+    fp[:, :32] = f.reshape(-1, 32)
+    Tp = torch.zeros(768, 2, device=dev)
+    Tp[:32] = T
+    logits = torch.empty(2 * 64, 2, device=dev)
+    ops.patch_scores([fp], Tp, logits, mode=1)
+    grid = logits.view(2, 8, 8, 2).permute(0, 3, 1, 2).contiguous()
+    out = torch.empty(2, 2, 40, 40, device=dev)
+    ops.blur_upsample(grid, out, ksize=0, sigma=0.0, softmax=True)
+    np.testing.assert_allclose(out.cpu().numpy(), o["sim_train"], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_anomaly_map_multi_level(dev, dt):
+    rng = np.random.default_rng(3)
+    B, g, C, S, L = 3, 24, 768, 336, 4
+    feats = [rng.standard_normal((B, g * g, C), dtype=np.float32) for _ in range(L)]
+    T = rng.standard_normal((C, 2)).astype(np.float32)
+    T /= np.linalg.norm(T, axis=0, keepdims=True)
+    lv = [torch.from_numpy(f.reshape(-1, C)).to(dev).to(dt) for f in feats]
+    feats = [t.float().cpu().numpy().reshape(B, g * g, C) for t in lv]  # oracle sees the same inputs
+    out = torch.empty(B, S, S, device=dev)
+    grid = torch.empty(B * g * g, device=dev)
+    ops.anomaly_map(lv, torch.from_numpy(T).to(dev), out, grid, g=g, ksize=7, sigma=1.0)
+    ref = R.anomaly_map([R.l2_normalize(f) for f in feats], T, S, "Industrial")
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-4, rtol=1e-5)
+
+
+def test_image_score(dev):
+    rng = np.random.default_rng(5)
+    B, P, C = 3, 576, 768
+    d = rng.standard_normal((B, P, C), dtype=np.float32)
+    T = rng.standard_normal((C, 2)).astype(np.float32)
+    D = torch.from_numpy(d.reshape(-1, C)).to(dev)
+    partial = torch.empty(B * 9 * C, device=dev)
+    det = torch.empty(B, C, device=dev)
+    score = torch.empty(B, device=dev)
+    ops.image_score(D, B, P, partial, det=det, T=torch.from_numpy(T).to(dev), score=score)
+    ref_det = R.l2_normalize(d).mean(1)
+    np.testing.assert_allclose(det.cpu().numpy(), ref_det, atol=1e-6, rtol=1e-5)
+    np.testing.assert_allclose(score.cpu().numpy(), R.image_score(ref_det, T), atol=1e-6)
