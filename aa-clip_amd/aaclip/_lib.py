@@ -39,7 +39,7 @@ SIGNATURES = {
     "aaclip_eot_ln": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "aaclip_anchor_reduce": [_P, _I, _I, _P, _I, _I, _P],
     "aaclip_l2_normalize": [_I, _I, _P, _L, _P, _L, _I, _I, _P],
-    "aaclip_patch_scores": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _P, _P],
+    "aaclip_patch_scores": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _I, _P, _P],
     "aaclip_blur_upsample": [_P, _P, _I, _I, _I, _I, _I, _F, _I, _P],
     "aaclip_anomaly_map": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P],
     "aaclip_image_score": [_I, _P, _L, _P, _I, _I, _I, _I, _P, _P, _P, _P],

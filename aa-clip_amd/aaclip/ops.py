@@ -200,7 +200,8 @@ def _level_array(levels):
     return arr
 
 
-def patch_scores(levels, T, out, *, normalize=True, mode=0):
+def patch_scores(levels, T, out, *, normalize=True, mode=0, group=0):
+    """mode 0: out[row] = sum_l (A1 + 1 - A0)/2; mode 1 (one level): out [B, 2, group] logits."""
     _dev(*levels, T, out)
     rows, C = levels[0].shape
     for t in levels:
@@ -212,9 +213,11 @@ def patch_scores(levels, T, out, *, normalize=True, mode=0):
     need = rows if mode == 0 else 2 * rows
     if out.numel() < need or out.dtype != torch.float32:
         raise ValueError("patch_scores output too small")
+    if mode == 1 and (group <= 0 or rows % group):
+        raise ValueError("mode 1 needs group = patches per image dividing the rows")
     arr = _level_array(levels)
     call("aaclip_patch_scores", dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(T), rows, C,
-         int(normalize), mode, _ptr(out), _stream())
+         int(normalize), mode, group, _ptr(out), _stream())
     return out
 
 

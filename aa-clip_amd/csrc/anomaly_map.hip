@@ -23,7 +23,8 @@ struct LevelPtrs {
 
 __global__ __launch_bounds__(256) void patch_scores_kernel(int in_dtype, LevelPtrs lv, int nl,
                                                            int64_t ld, const float* T, int rows,
-                                                           int normalize, int mode, float* out) {
+                                                           int normalize, int mode, int group,
+                                                           float* out) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -78,8 +79,9 @@ __global__ __launch_bounds__(256) void patch_scores_kernel(int in_dtype, LevelPt
       if (mode == 0) {
         acc += (A1 + 1.0f - A0) / 2.0f;
       } else if (lane == 0) {
-        out[2 * (size_t)row] = A0;
-        out[2 * (size_t)row + 1] = A1;
+        const size_t base = (size_t)(row / group) * 2 * group + row % group;
+        out[base] = A0;
+        out[base + group] = A1;
       }
     }
   }
@@ -253,10 +255,12 @@ Gauss gaussian_weights(int k, float sigma) {
 
 extern "C" int aaclip_patch_scores(int in_dtype, const void* const* levels, int n_levels,
                                    int64_t ld, const float* T, int rows, int channels,
-                                   int normalize, int mode, float* out, void* stream) {
+                                   int normalize, int mode, int group, float* out,
+                                   void* stream) {
   AACLIP_REQUIRE(in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16);
   AACLIP_REQUIRE(levels && T && out && rows >= 0 && channels == 768 && ld >= channels && ld % 4 == 0);
   AACLIP_REQUIRE(n_levels >= 1 && n_levels <= kMaxLevels && (mode == 0 || (mode == 1 && n_levels == 1)));
+  AACLIP_REQUIRE(mode == 0 || (group > 0 && rows % group == 0));
   LevelPtrs lv{};
   for (int i = 0; i < n_levels; ++i) {
     AACLIP_REQUIRE(levels[i] != nullptr);
@@ -264,7 +268,7 @@ extern "C" int aaclip_patch_scores(int in_dtype, const void* const* levels, int 
   }
   if (rows == 0) return AACLIP_OK;
   patch_scores_kernel<<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
-      in_dtype, lv, n_levels, ld, T, rows, normalize, mode, out);
+      in_dtype, lv, n_levels, ld, T, rows, normalize, mode, mode == 1 ? group : 1, out);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -292,7 +296,7 @@ extern "C" int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n
                                   float* out, void* stream) {
   AACLIP_REQUIRE(grid_ws && batch > 0);
   int rc = aaclip_patch_scores(in_dtype, levels, n_levels, ld, T, batch * g * g, channels,
-                               normalize, 0, grid_ws, stream);
+                               normalize, 0, 0, grid_ws, stream);
   if (rc) return rc;
   return aaclip_blur_upsample(grid_ws, out, batch, 1, g, out_size, ksize, sigma, 0, stream);
 }

@@ -1,0 +1,131 @@
+"""Drop-in for the reference forward_utils.py entry points of the eval path.
+
+  get_adapted_single_class_text_embedding / get_adapted_text_embedding
+      forward_utils.py:138-162, :185-192 — prompt ensemble -> T [768, 2]; the
+      encoder runs on the HIP text engine, the normalise/mean/normalise
+      reduction in the aaclip_anchor_reduce kernel.
+  calculate_similarity_map   forward_utils.py:196-216 — aaclip_patch_scores +
+      aaclip_blur_upsample (test: (A1+1-A0)/2 -> Gaussian -> bilinear;
+      train: bilinear -> softmax over the two anchors).
+  anomaly_map_multilevel     the fused form of test.py:86-93 (all levels in one
+      stream kernel, level sum before blur+upsample).
+  metrics_eval               forward_utils.py:233-280, host-side (numpy/sklearn,
+      as in the reference; the §8(f)-1 "next" row moves it on device).
+Training losses and visualize() (cv2) are out of scope.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from aaclip import ops
+from aaclip.engine import _blur_for
+from dataset.constants import CLASS_NAMES, PROMPTS, REAL_NAMES
+from model.tokenizer import tokenize
+
+prompt = PROMPTS
+prompt_normal = prompt["prompt_normal"]
+prompt_abnormal = prompt["prompt_abnormal"]
+prompt_state = [prompt_normal, prompt_abnormal]
+prompt_templates = prompt["prompt_templates"]
+
+
+def _sentences(real_name):
+    out = []
+    for states in prompt_state:
+        out.append([tpl.format(s.format(real_name)) for s in states for tpl in prompt_templates])
+    return out
+
+
+def get_adapted_single_class_text_embedding(model, dataset_name, class_name, device):
+    if class_name == "object":
+        real_name = class_name
+    else:
+        assert class_name in CLASS_NAMES[dataset_name], (
+            f"class_name {class_name} not found; available class_names: {CLASS_NAMES[dataset_name]}")
+        real_name = REAL_NAMES[dataset_name][class_name]
+    device = torch.device(device)
+    T = None
+    for col, sentences in enumerate(_sentences(real_name)):
+        emb = model.encode_text(tokenize(sentences).to(device)).to(torch.float32).contiguous()
+        if T is None:
+            T = torch.empty(emb.shape[1], 2, device=emb.device, dtype=torch.float32)
+        ops.anchor_reduce(emb, T, col)
+    return T.to(device)
+
+
+def get_adapted_text_embedding(model, dataset_name, device):
+    return {c: get_adapted_single_class_text_embedding(model, dataset_name, c, device)
+            for c in CLASS_NAMES[dataset_name]}
+
+
+def calculate_similarity_map(patch_features, epoch_text_feature, img_size, test=False, domain="Medical"):
+    """[B, L, C] features x [C, 2] anchors -> [B, 1, S, S] (test) / [B, 2, S, S] (train)."""
+    B, L, C = patch_features.shape
+    H = int(np.sqrt(L))
+    if H * H != L:
+        raise ValueError("patch count must be a square")
+    Cn = epoch_text_feature.shape[1]
+    if test:
+        assert Cn == 2
+    elif Cn != 2:
+        raise NotImplementedError("only the 2-anchor (normal, abnormal) form is on the path")
+    f = patch_features.reshape(B * L, C)
+    if f.dtype not in (torch.float32, torch.bfloat16):
+        f = f.float()
+    f = f.contiguous()
+    T = epoch_text_feature.to(f.device, torch.float32).contiguous()
+    dev = f.device
+    if test:
+        grid = torch.empty(B, 1, H, H, device=dev, dtype=torch.float32)
+        ops.patch_scores([f], T, grid, normalize=False, mode=0)
+        k, s = _blur_for(domain)
+        out = torch.empty(B, 1, img_size, img_size, device=dev, dtype=torch.float32)
+        return ops.blur_upsample(grid, out, ksize=k, sigma=s)
+    grid = torch.empty(B, 2, H, H, device=dev, dtype=torch.float32)
+    ops.patch_scores([f], T, grid, normalize=False, mode=1, group=L)
+    out = torch.empty(B, 2, img_size, img_size, device=dev, dtype=torch.float32)
+    return ops.blur_upsample(grid, out, ksize=0, sigma=0.0, softmax=True)
+
+
+def anomaly_map_multilevel(patch_features, epoch_text_feature, img_size, domain="Industrial", normalize=False):
+    """sum_l calculate_similarity_map(f_l, T, S, test=True, domain) -> [B, S, S] in one pass."""
+    B, L, C = patch_features[0].shape
+    g = int(np.sqrt(L))
+    lv = [f.reshape(B * L, C).contiguous() for f in patch_features]
+    T = epoch_text_feature.to(lv[0].device, torch.float32).contiguous()
+    out = torch.empty(B, img_size, img_size, device=lv[0].device, dtype=torch.float32)
+    grid = torch.empty(B * L, device=lv[0].device, dtype=torch.float32)
+    k, s = _blur_for(domain)
+    return ops.anomaly_map(lv, T, out, grid, g=g, ksize=k, sigma=s, normalize=normalize)
+
+
+def metrics_eval(pixel_label: np.ndarray, image_label: np.ndarray, pixel_preds: np.ndarray,
+                 image_preds: np.ndarray, class_names: str, domain: str):
+    from sklearn.metrics import average_precision_score, roc_auc_score
+    if pixel_preds.max() != 1:
+        pixel_preds = (pixel_preds - pixel_preds.min()) / (pixel_preds.max() - pixel_preds.min())
+    if image_preds.max() != 1:
+        image_preds = (image_preds - image_preds.min()) / (image_preds.max() - image_preds.min())
+    pmax_pred = pixel_preds.max(axis=(1, 2))
+    if domain != "Medical":
+        image_preds = pmax_pred * 0.5 + image_preds * 0.5
+    else:
+        image_preds = pmax_pred
+    pixel_label = pixel_label.flatten()
+    pixel_preds = pixel_preds.flatten()
+    zero_pixel_auc = roc_auc_score(pixel_label, pixel_preds)
+    zero_pixel_ap = average_precision_score(pixel_label, pixel_preds)
+    if image_label.max() != image_label.min():
+        agg_image_auc = roc_auc_score(image_label.flatten(), image_preds.flatten())
+        agg_image_ap = average_precision_score(image_label.flatten(), image_preds.flatten())
+    else:
+        agg_image_auc = 0
+        agg_image_ap = 0
+    return {"class name": class_names, "pixel AUC": round(zero_pixel_auc, 4) * 100,
+            "pixel AP": round(zero_pixel_ap, 4) * 100, "image AUC": round(agg_image_auc, 4) * 100,
+            "image AP": round(agg_image_ap, 4) * 100}
+
+
+def visualize(pixel_label, pixel_preds, file_names, save_dir, dataset_name, class_name):
+    raise NotImplementedError("visualize() writes cv2 overlays; cv2 is not in this image and it is not on the path")

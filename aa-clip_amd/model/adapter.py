@@ -1,0 +1,100 @@
+"""AdaptedCLIP — drop-in for reference model/adapter.py:6-145.
+
+Same constructor, attributes (`clipmodel`, `image_encoder`, `image_adapter`
+ModuleDict{layer_adapters, seg_proj, det_proj}, `text_adapter` ModuleList,
+`t_w`, `i_w`, `levels`, ...) and state-dict keys. `forward` / `encode_text`
+run on the MI355X engines (aaclip.engine) built from the module's current
+parameters; the packed device copies are rebuilt whenever a parameter changes
+(load_state_dict, in-place edits: tracked by tensor version counters).
+
+Compute dtype of the visual tower: bf16 MFMA by default (`compute_dtype=
+torch.float32` selects the fp32-MFMA parity mode; env AACLIP_DTYPE=fp32 too).
+The text tower always runs fp32 (once per dataset, <1% of the work).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+from torch import nn
+
+from .adapter_modules import SimpleAdapter, SimpleProj
+
+
+def param_signature(module: nn.Module, prefix_excl: str | None = None):
+    return tuple((n, p.data_ptr(), p._version) for n, p in module.state_dict(keep_vars=True).items()
+                 if prefix_excl is None or not n.startswith(prefix_excl))
+
+
+def _default_dtype():
+    v = os.environ.get("AACLIP_DTYPE", "bf16").lower()
+    return torch.float32 if v in ("fp32", "float32", "f32") else torch.bfloat16
+
+
+class AdaptedCLIP(nn.Module):
+    def __init__(self, clip_model, text_adapt_weight: float = 0.1, image_adapt_weight: float = 0.1,
+                 text_adapt_until: int = 3, image_adapt_until: int = 6, levels: list = [6, 12, 18, 24],
+                 relu: bool = True, compute_dtype: torch.dtype | None = None, **kwargs):
+        super().__init__()
+        self.clipmodel = clip_model
+        self.image_encoder = clip_model.visual
+        self.text_adapt_until = text_adapt_until
+        self.image_adapt_until = image_adapt_until
+        self.t_w = text_adapt_weight
+        self.i_w = image_adapt_weight
+        self.levels = list(levels)
+        self.compute_dtype = compute_dtype or _default_dtype()
+        width = clip_model.visual.conv1.weight.shape[0]
+        embed = clip_model.visual.output_dim
+        twidth = clip_model.transformer.width
+        layer_adapters = nn.ModuleList([SimpleAdapter(width, width) for _ in range(image_adapt_until)])
+        seg_proj = nn.ModuleList([SimpleProj(width, embed, relu) for _ in range(len(levels))])
+        det_proj = SimpleProj(width, embed, relu)
+        self.image_adapter = nn.ModuleDict({"layer_adapters": layer_adapters, "seg_proj": seg_proj,
+                                            "det_proj": det_proj})
+        self.text_adapter = nn.ModuleList([SimpleAdapter(twidth, twidth) for _ in range(text_adapt_until)]
+                                          + [SimpleProj(twidth, embed, relu=True)])
+        self._init_weights_()
+        self._vis = None
+        self._vis_sig = None
+
+    def _init_weights_(self):
+        for p in self.image_adapter.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_uniform_(p)
+        for p in self.text_adapter.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_uniform_(p)
+
+    # ------------------------------------------------------------------ engines
+    def visual_engine(self):
+        from aaclip.engine import VisualEngine
+        sig = (param_signature(self.image_encoder), param_signature(self.image_adapter), tuple(self.levels),
+               self.image_adapt_until, self.i_w, self.compute_dtype)
+        if self._vis is None or self._vis_sig != sig:
+            vp = {"visual." + k: v for k, v in self.image_encoder.state_dict().items()}
+            self._vis = VisualEngine(vp, self.image_adapter.state_dict(), levels=self.levels,
+                                     image_adapt_until=self.image_adapt_until, image_adapt_weight=self.i_w,
+                                     dtype=self.compute_dtype)
+            self._vis_sig = sig
+        return self._vis
+
+    # ------------------------------------------------------------------ API
+    def forward_original(self, x, modality="visual"):
+        if modality != "visual":
+            raise ValueError("modality must be visual")
+        raise NotImplementedError("forward_original (plain CLIP patch tokens) is not on the AA-CLIP eval path")
+
+    def forward(self, x):
+        """(list[len(levels)] of [B, P, 768] unit-norm patch features, det [B, 768])."""
+        return self.visual_engine().forward(x)
+
+    def predict(self, x, text_features, domain="Industrial"):
+        """Fused test path (test.py:80-93): (anomaly map [B,S,S], image score [B]), fp32."""
+        return self.visual_engine().predict(x, text_features, domain)
+
+    def encode_text(self, text, adapt_text=True):
+        if not adapt_text:
+            return self.clipmodel.encode_text(text)
+        eng = self.clipmodel.text_engine(self.text_adapter.state_dict(), self.text_adapt_until, self.t_w)
+        return eng.encode(text)

@@ -1,0 +1,141 @@
+"""Evaluation harness — the counterpart of the reference test.py (same flags,
+same flow, same outputs), running AdaptedCLIP on the MI355X kernels.
+
+    python test.py --dataset MVTec --img_size 336 --save_path ckpt/...     (needs weights + data)
+    python test.py --dataset synthetic --allow_random_init --img_size 336  (C1: no files needed)
+
+Differences from the reference, all on the host side:
+  * the per-batch loop calls the fused AdaptedCLIP.predict (map + score in one
+    device pass) and keeps results on the device until the class is done
+    (the reference syncs twice per batch, test.py:85,93);
+  * checkpoints load with torch.load(weights_only=True);
+  * --allow_random_init / --dataset synthetic run without the OpenAI weights.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import sys
+from glob import glob
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from dataset import DOMAINS, get_dataset  # noqa: E402
+from forward_utils import get_adapted_text_embedding, metrics_eval, visualize  # noqa: E402
+from model.adapter import AdaptedCLIP  # noqa: E402
+from model.clip import create_model  # noqa: E402
+from utils import setup_seed  # noqa: E402
+
+
+def get_predictions(model, class_text_embeddings, test_loader, device, img_size, dataset="MVTec"):
+    masks, labels, preds, preds_image, file_names = [], [], [], [], []
+    for input_data in test_loader:
+        image = input_data["image"].to(device, non_blocking=True)
+        class_name = input_data["class_name"]
+        assert len(set(class_name)) == 1, "mixed class not supported"
+        masks.append(input_data["mask"].cpu().numpy())
+        labels.append(np.asarray(input_data["label"]))
+        file_names.extend(input_data["file_name"])
+        pmap, score = model.predict(image, class_text_embeddings, DOMAINS[dataset])
+        preds.append(pmap.clone())
+        preds_image.append(score.clone())
+    preds = torch.cat(preds).cpu().numpy()
+    preds_image = torch.cat(preds_image).cpu().numpy()
+    return (np.concatenate(masks, axis=0), np.concatenate(labels, axis=0), preds, preds_image, file_names)
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(description="Testing")
+    parser.add_argument("--model_name", type=str, default="ViT-L-14-336", help="ViT-L-14-336")
+    parser.add_argument("--img_size", type=int, default=518)
+    parser.add_argument("--relu", action="store_true")
+    parser.add_argument("--dataset", type=str, default="MVTec")
+    parser.add_argument("--shot", type=int, default=4)
+    parser.add_argument("--batch_size", type=int, default=32)
+    parser.add_argument("--seed", type=int, default=111)
+    parser.add_argument("--save_path", type=str, default="ckpt/baseline")
+    parser.add_argument("--visualize", action="store_true")
+    parser.add_argument("--text_norm_weight", type=float, default=0.1)
+    parser.add_argument("--text_adapt_weight", type=float, default=0.1)
+    parser.add_argument("--image_adapt_weight", type=float, default=0.1)
+    parser.add_argument("--text_adapt_until", type=int, default=3)
+    parser.add_argument("--image_adapt_until", type=int, default=6)
+    # build-only flags
+    parser.add_argument("--allow_random_init", action="store_true",
+                        help="run on random-init CLIP + adapters when no checkpoints exist")
+    parser.add_argument("--synthetic_n", type=int, default=16)
+    parser.add_argument("--compute_dtype", type=str, default="bf16", choices=["bf16", "fp32"])
+    args = parser.parse_args(argv)
+
+    setup_seed(args.seed)
+    os.makedirs(args.save_path, exist_ok=True)
+    logger = logging.getLogger(__name__)
+    logging.basicConfig(filename=os.path.join(args.save_path, "test.log"), encoding="utf-8", level=logging.INFO)
+    logger.info("args: %s", vars(args))
+    if not torch.cuda.is_available():
+        raise RuntimeError("the AA-CLIP MI355X build needs a GPU (no CPU path)")
+    device = torch.device("cuda:0")
+
+    clip_model = create_model(model_name=args.model_name, img_size=args.img_size, device=device,
+                              pretrained=None if args.allow_random_init else "openai",
+                              require_pretrained=not args.allow_random_init,
+                              force_image_size=args.img_size if args.allow_random_init else None)
+    clip_model.eval()
+    model = AdaptedCLIP(clip_model=clip_model, text_adapt_weight=args.text_adapt_weight,
+                        image_adapt_weight=args.image_adapt_weight, text_adapt_until=args.text_adapt_until,
+                        image_adapt_until=args.image_adapt_until, relu=args.relu,
+                        compute_dtype=torch.float32 if args.compute_dtype == "fp32" else torch.bfloat16).to(device)
+    model.eval()
+
+    text_file = glob(args.save_path + "/text_adapter.pth")
+    if len(text_file) > 0:
+        checkpoint = torch.load(text_file[0], map_location="cpu", weights_only=True)
+        model.text_adapter.load_state_dict(checkpoint["text_adapter"])
+        adapt_text = True
+    else:
+        adapt_text = False
+
+    files = sorted(glob(args.save_path + "/image_adapter_*.pth"))
+    if not files and args.allow_random_init:
+        files = [None]
+    assert len(files) > 0, "image adapter checkpoint not found"
+    from pandas import DataFrame, Series
+    for file in files:
+        if file is not None:
+            checkpoint = torch.load(file, map_location="cpu", weights_only=True)
+            model.image_adapter.load_state_dict(checkpoint["image_adapter"])
+            test_epoch = checkpoint["epoch"]
+        else:
+            test_epoch = -1
+        logger.info("-----------------------------------------------")
+        logger.info("load model from epoch %d", test_epoch)
+        logger.info("-----------------------------------------------")
+        image_datasets = get_dataset(args.dataset, args.img_size, None, args.shot, "test", logger=logger,
+                                     synthetic_n=args.synthetic_n)
+        with torch.no_grad():
+            text_embeddings = get_adapted_text_embedding(model if adapt_text else clip_model, args.dataset, device)
+        df = DataFrame(columns=["class name", "pixel AUC", "pixel AP", "image AUC", "image AP"])
+        for class_name, image_dataset in image_datasets.items():
+            loader = torch.utils.data.DataLoader(image_dataset, batch_size=args.batch_size, shuffle=False,
+                                                 num_workers=4, pin_memory=True)
+            with torch.no_grad():
+                masks, labels, preds, preds_image, file_names = get_predictions(
+                    model=model, class_text_embeddings=text_embeddings[class_name], test_loader=loader,
+                    device=device, img_size=args.img_size, dataset=args.dataset)
+            if args.visualize:
+                visualize(masks, preds, file_names, args.save_path, args.dataset, class_name=class_name)
+            result = metrics_eval(masks, labels, preds, preds_image, class_name, domain=DOMAINS[args.dataset])
+            df.loc[len(df)] = Series(result)
+        df.loc[len(df)] = df.drop(columns=["class name"]).mean()
+        df.loc[len(df) - 1, "class name"] = "Average"
+        logger.info("final results:\n%s", df.to_string(index=False, justify="center"))
+        print(df.to_string(index=False, justify="center"))
+    return df
+
+
+if __name__ == "__main__":
+    main()

@@ -147,13 +147,14 @@ int aaclip_l2_normalize(int in_dtype, int out_dtype, const void* x, int64_t ldx,
  * of n_levels device pointers, each [rows, channels], row stride ld):
  *   f_hat = normalize ? f/max(||f||,1e-12) : f;  A_c = 100 * f_hat . T[:, c]
  *   mode 0 (test): out[row] = sum_l (A_1 + 1 - A_0) / 2
- *   mode 1 (train, n_levels == 1): out[row*2 + c] = A_c
- * T: [channels, 2] fp32. Replaces: forward_utils.py:199-207 (+ the level sum of
+ *   mode 1 (train, n_levels == 1): out[b, c, p] = A_c with b = row / group,
+ *          p = row % group (channel-major [B, 2, group], ready for blur_upsample)
+ * T: [channels, 2] fp32. group = patches per image (mode 1 only). Replaces: forward_utils.py:199-207 (+ the level sum of
  * test.py:93, moved before the blur/upsample: both are linear).
  */
 int aaclip_patch_scores(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
                         const float* T, int rows, int channels, int normalize, int mode,
-                        float* out, void* stream);
+                        int group, float* out, void* stream);
 
 /*
  * Gaussian blur (kornia 0.6.9 gaussian_blur2d, reflect border, separable;

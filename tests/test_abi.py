@@ -1,0 +1,53 @@
+"""The C-ABI library loads on the CPU host and exports every symbol that
+include/aaclip.h declares; host-side argument validation rejects bad calls
+before any launch (no kernel runs here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from aaclip import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared():
+    src = open(os.path.join(ROOT, "include", "aaclip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(aaclip_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_matches_binding_table():
+    assert declared() == sorted(_lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.lib()
+    for name in declared():
+        assert hasattr(lib, name), name
+    assert lib.aaclip_abi_version() == _lib.ABI_VERSION
+    assert lib.aaclip_arch() == b"gfx950"
+
+
+def test_argument_validation_rejects_without_launch():
+    lib = _lib.lib()
+    # null operands / bad dtype / unsupported shapes return AACLIP_ERR_ARG (=1)
+    assert lib.aaclip_gemm(5, 0, 8, 128, 64, None, 64, None, 64, None, 128, 0, None, None, 0, None, 0, 0, 0, 0, None) == 1
+    assert lib.aaclip_attention(1, None, None, 1, 8, 1, 64, 0, None) == 1
+    assert lib.aaclip_attention(1, ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 8, 1, 128, 0, None) == 1  # head_dim
+    assert lib.aaclip_layernorm(0, None, 512, None, None, None, 512, 4, 512, None) == 1
+    assert lib.aaclip_blur_upsample(None, None, 1, 3, 24, 336, 7, 1.0, 0, None) == 1
+    lv = (ctypes.c_void_p * 1)(16)
+    assert lib.aaclip_patch_scores(1, lv, 1, 768, ctypes.c_void_p(16), 4, 512, 1, 0, 0, ctypes.c_void_p(16), None) == 1
+    with pytest.raises(RuntimeError):
+        _lib.check(1, "aaclip_gemm")
+
+
+def test_product_path_does_not_import_the_oracle():
+    pkg = os.path.join(ROOT, "aa-clip_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, flags=re.M), f

@@ -201,9 +201,8 @@ def test_similarity_map_train_golden(dev, golden):
     fp[:, :32] = f.reshape(-1, 32)
     Tp = torch.zeros(768, 2, device=dev)
     Tp[:32] = T
-    logits = torch.empty(2 * 64, 2, device=dev)
-    ops.patch_scores([fp], Tp, logits, mode=1)
-    grid = logits.view(2, 8, 8, 2).permute(0, 3, 1, 2).contiguous()
+    grid = torch.empty(2, 2, 8, 8, device=dev)
+    ops.patch_scores([fp], Tp, grid, mode=1, group=64)
     out = torch.empty(2, 2, 40, 40, device=dev)
     ops.blur_upsample(grid, out, ksize=0, sigma=0.0, softmax=True)
     np.testing.assert_allclose(out.cpu().numpy(), o["sim_train"], atol=1e-5, rtol=1e-5)
