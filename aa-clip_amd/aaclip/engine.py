@@ -95,8 +95,8 @@ class VisualEngine:
         self._ws = {}
 
     # ------------------------------------------------------------------ workspace
-    def _workspace(self, B: int, S: int):
-        key = (B, S)
+    def _workspace(self, B: int, S: int, slot: int = 0):
+        key = (B, S, slot)
         if key in self._ws:
             return self._ws[key]
         g = S // PATCH
@@ -122,19 +122,21 @@ class VisualEngine:
             det=e(B, EMBED, dt=torch.float32), score=e(B, dt=torch.float32),
             map=e(B, S, S, dt=torch.float32),
         )
-        self._ws = {key: ws}  # keep one batch shape resident
+        # keep only the workspaces of the current (batch, size) resident
+        self._ws = {k: v for k, v in self._ws.items() if k[:2] == key[:2]}
+        self._ws[key] = ws
         return ws
 
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
-    def forward_raw(self, x: torch.Tensor):
+    def forward_raw(self, x: torch.Tensor, slot: int = 0):
         """Run the visual tower; returns (seg_raw list of [B*P, 768] views,
         det_raw [B*P, 768] view, workspace). Rows are unnormalised projections."""
         if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != x.shape[3] or x.shape[2] % PATCH:
             raise ValueError("input must be [B, 3, S, S] with S a multiple of 14")
         x = x.to(self.device, torch.float32).contiguous()
         B, _, S, _ = x.shape
-        ws = self._workspace(B, S)
+        ws = self._workspace(B, S, slot)
         P, n_tok = ws["P"], ws["n_tok"]
         X, H = ws["x"], ws["h"]
         ops.im2col(x, ws["cols"], PATCH)
@@ -185,17 +187,53 @@ class VisualEngine:
         ops.image_score(det_raw, B, P, ws["partial"], det=det)
         return out, det
 
+    def _chunk_streams(self, n: int):
+        if len(getattr(self, "_streams", [])) < n:
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(n)]
+        return self._streams[:n]
+
     @torch.no_grad()
-    def predict(self, x: torch.Tensor, T: torch.Tensor, domain: str = "Industrial"):
+    def predict(self, x: torch.Tensor, T: torch.Tensor, domain: str = "Industrial", streams: int = 1):
         """Fused test path: (anomaly map [B,S,S] fp32, image score [B] fp32),
-        = test.py:80-93 with the level sum ahead of blur+upsample."""
-        seg_raw, det_raw, ws = self.forward_raw(x)
+        = test.py:80-93 with the level sum ahead of blur+upsample.
+
+        streams > 1 splits the batch into that many image chunks, each run on its
+        own HIP stream with its own workspace: the GEMM tails of one chunk
+        (tile counts that leave CUs idle in the last wave) are filled by another
+        chunk's tiles. Outputs land in one [B,S,S] / [B] buffer."""
         B, S = x.shape[0], x.shape[-1]
         T = T.to(self.device, torch.float32).contiguous()
         k, s = _blur_for(domain)
-        ops.anomaly_map(seg_raw, T, ws["map"], ws["grid"], g=ws["g"], ksize=k, sigma=s)
-        ops.image_score(det_raw, B, ws["P"], ws["partial"], det=ws["det"], T=T, score=ws["score"])
-        return ws["map"], ws["score"]
+        streams = max(1, min(int(streams), B))
+        if streams == 1:
+            seg_raw, det_raw, ws = self.forward_raw(x)
+            ops.anomaly_map(seg_raw, T, ws["map"], ws["grid"], g=ws["g"], ksize=k, sigma=s)
+            ops.image_score(det_raw, B, ws["P"], ws["partial"], det=ws["det"], T=T, score=ws["score"])
+            return ws["map"], ws["score"]
+        key = ("out", B, S)
+        if key not in self._ws:
+            self._ws[key] = (torch.empty(B, S, S, device=self.device), torch.empty(B, device=self.device))
+        out_map, out_score = self._ws[key]
+        x = x.to(self.device, torch.float32).contiguous()
+        bounds = [(B * i) // streams for i in range(streams + 1)]
+        main = torch.cuda.current_stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        done = []
+        for i, st in enumerate(self._chunk_streams(streams)):
+            b0, b1 = bounds[i], bounds[i + 1]
+            with torch.cuda.stream(st):
+                st.wait_event(ready)
+                seg_raw, det_raw, ws = self.forward_raw(x[b0:b1], slot=i)
+                ops.anomaly_map(seg_raw, T, out_map[b0:b1], ws["grid"], g=ws["g"], ksize=k, sigma=s)
+                ops.image_score(det_raw, b1 - b0, ws["P"], ws["partial"], det=ws["det"], T=T,
+                                score=out_score[b0:b1])
+                ev = torch.cuda.Event()
+                ev.record(st)
+                done.append(ev)
+        for ev in done:
+            main.wait_event(ev)
+        return out_map, out_score
 
 
 class TextEngine:

@@ -5,7 +5,8 @@
 // v_mfma_f32_16x16x32_bf16 is 8 consecutive K values = one 16-byte ds_read_b128.
 //
 // bf16 kernel (perf path):
-//   * block tile BM x BN x 64, 8 waves (512 threads), wave tile (BM/WM) x (BN/WN)
+//   * block tile BM x BN x 64, 8 waves (512 threads), wave tile (BM/WM) x (BN/WN);
+//     default 320x256 (wave tile 160x64 = 10x4 MFMA tiles, 144 KiB LDS double buffer)
 //   * global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
 //     instruction = 8 rows of 128 B). The LDS image is lane-linear, so the bank
 //     swizzle (16-B chunk c of row r stored at chunk c ^ (r & 7)) is applied on
@@ -46,6 +47,23 @@ __device__ __forceinline__ float gelu_erf(float v) {
   return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
 }
 
+// GELU for the bf16 path: 1 + erf(z) through erfc(|z|) from Abramowitz-Stegun
+// 7.1.26 (|error| <= 1.5e-7, far below bf16's 2^-9 output rounding): one rcp,
+// one exp and a degree-5 polynomial instead of OCML's branchy erff, which
+// dominated the c_fc epilogue. For z < 0 the erfc form keeps GELU's small
+// negative tail accurate (no 1 - (1 - e) cancellation).
+__device__ __forceinline__ float gelu_fast(float v) {
+  const float z = v * 0.70710678118654752440f;
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float erfc_az = t * p * __expf(-az * az);
+  return 0.5f * v * (z >= 0.f ? 2.0f - erfc_az : erfc_az);
+}
+
 // Epilogue on one element C[m, n] (m < M checked by the caller).
 __device__ __forceinline__ void epilogue_store1(const GemmArgs& a, int m, int n, float v) {
   const int orow = remap_row(a, m);
@@ -66,7 +84,7 @@ __device__ __forceinline__ void epilogue_store4(const GemmArgs& a, int m, int n,
   if (a.epi & AACLIP_EPI_BIAS) v += *(const float4_t*)(a.bias + n);
   if (a.epi & AACLIP_EPI_GELU)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
+    for (int j = 0; j < 4; ++j) v[j] = gelu_fast(v[j]);
   if (a.epi & AACLIP_EPI_LEAKY)
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = v[j] >= 0.f ? v[j] : 0.01f * v[j];
@@ -226,6 +244,180 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   }
 }
 
+// ============================================================== bf16 MFMA, 4-phase pipeline
+// 256x256x64 tile, 8 waves (2 along M x 4 along N, wave tile 128x64 = 8x4
+// MFMA tiles). Each K-tile is computed in 4 phases, one 64x32 quadrant of the
+// wave tile (16 MFMAs) per phase:
+//   P1 (A lo, B lo)   P2 (A lo, B hi)   P3 (A hi, B hi)   P4 (A hi, B lo)
+// The LDS image of one K-tile is cut into 4 regions of 128 rows x 128 B by the
+// phase that first reads them, across waves:
+//   R1 = A lo rows of both M-halves, R2 = B lo rows of all 4 N-quarters,
+//   R3 = B hi rows, R4 = A hi rows.
+// Phase p of K-tile t issues region R_p of K-tile t+1 (2 LDS-DMA instructions
+// per wave) into the other buffer, then runs its MFMAs, then waits with a
+// COUNTED vmcnt(4) — two regions stay in flight across the barrier — before the
+// one raw s_barrier of the phase. Every region therefore has >= 3 phases between
+// issue and first read (P1->P1, P2->P1, P3->P2, P4->P3), and its buffer slot was
+// last read >= 1 barrier earlier (R1: P2, R2: P4, R3: P2, R4: P3 of tile t-1).
+// The last K-tile drains with vmcnt(0).
+__device__ __forceinline__ int reg_a_row(int q, int hi) {  // region row -> tile row (A)
+  return (q >> 6) * 128 + hi * 64 + (q & 63);
+}
+__device__ __forceinline__ int reg_b_row(int q, int hi) {  // region row -> tile row (B / n)
+  return (q >> 5) * 64 + hi * 32 + (q & 31);
+}
+
+#define VM_WAIT_BARRIER(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_barrier" ::: "memory")
+
+__global__ __launch_bounds__(512) void gemm_bf16_4ph_kernel(GemmArgs a) {
+  constexpr int REG = 128 * 128;      // bytes per region
+  constexpr int STAGE = 4 * REG;      // R1 R2 R3 R4
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  int tm, tn;
+  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const uint16_t* __restrict__ Ag = (const uint16_t*)a.A;
+  const uint16_t* __restrict__ Wg = (const uint16_t*)a.W;
+
+  // DMA sources: region rows q = (piece)*8 + lane/8 for pieces wid and wid+8;
+  // physical chunk lane%8 holds logical chunk (lane%8) ^ (q&7).
+  const uint16_t* src[4][2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = (wid + 8 * k) * 8 + (lane >> 3);
+    const int c = ((lane & 7) ^ (q & 7)) * 8;
+    src[0][k] = Ag + (size_t)min(m0 + reg_a_row(q, 0), a.M - 1) * a.lda + c;  // R1
+    src[1][k] = Wg + (size_t)(n0 + reg_b_row(q, 0)) * a.ldw + c;              // R2
+    src[2][k] = Wg + (size_t)(n0 + reg_b_row(q, 1)) * a.ldw + c;              // R3
+    src[3][k] = Ag + (size_t)min(m0 + reg_a_row(q, 1), a.M - 1) * a.lda + c;  // R4
+  }
+#define ISSUE_REGION(r, kt, buf)                                                             \
+  do {                                                                                       \
+    char* dst_ = smem + (buf) * STAGE + (r) * REG;                                           \
+    const int ko_ = (kt) * 64;                                                               \
+    __builtin_amdgcn_global_load_lds((const void*)(src[r][0] + ko_), LDS_PTR(dst_ + wid * 1024), 16, 0, 0); \
+    __builtin_amdgcn_global_load_lds((const void*)(src[r][1] + ko_), LDS_PTR(dst_ + (wid + 8) * 1024), 16, 0, 0); \
+  } while (0)
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // fragment byte offsets inside a region (row q, logical chunk kk*4+fq)
+  auto roff = [&](int q, int kk) { return q * 128 + (((kk * 4 + fq) ^ (q & 7)) << 4); };
+  int aoff[4][2], boff[2][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) aoff[i][kk] = roff(wm * 64 + i * 16 + fr, kk);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) boff[j][kk] = roff(wn * 32 + j * 16 + fr, kk);
+
+  float4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / 64;
+  ISSUE_REGION(0, 0, 0);
+  ISSUE_REGION(1, 0, 0);
+  ISSUE_REGION(2, 0, 0);
+  ISSUE_REGION(3, 0, 0);
+  VM_WAIT_BARRIER(0);
+
+  bf16x8_t af[4][2], bf[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * STAGE;
+    const bool more = kt + 1 < nk;
+    const int nb = (kt + 1) & 1;
+    // ---- P1: A lo (R1) x B lo (R2)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = *(const bf16x8_t*)(st + REG + boff[j][kk]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = *(const bf16x8_t*)(st + aoff[i][kk]);
+    if (more) ISSUE_REGION(0, kt + 1, nb);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[i][j], 0, 0, 0);
+    if (more) VM_WAIT_BARRIER(4); else VM_WAIT_BARRIER(0);
+    // ---- P2: A lo (regs) x B hi (R3)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = *(const bf16x8_t*)(st + 2 * REG + boff[j][kk]);
+    if (more) ISSUE_REGION(1, kt + 1, nb);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[i][2 + j], 0, 0, 0);
+    if (more) VM_WAIT_BARRIER(4); else VM_WAIT_BARRIER(0);
+    // ---- P3: A hi (R4) x B hi (regs)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = *(const bf16x8_t*)(st + 3 * REG + aoff[i][kk]);
+    if (more) ISSUE_REGION(2, kt + 1, nb);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[4 + i][2 + j], 0, 0, 0);
+    if (more) VM_WAIT_BARRIER(6); else VM_WAIT_BARRIER(0);
+    // ---- P4: A hi (regs) x B lo (R2 re-read)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = *(const bf16x8_t*)(st + REG + boff[j][kk]);
+    if (more) ISSUE_REGION(3, kt + 1, nb);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[4 + i][j], 0, 0, 0);
+    if (more) VM_WAIT_BARRIER(4); else VM_WAIT_BARRIER(0);
+  }
+#undef ISSUE_REGION
+
+  // ---- epilogue (LDS free: every DMA retired by the final vmcnt(0) + barrier)
+  constexpr int TN = 64, EP_LD = TN + 4, F4_PER_ROW = TN / 4;
+  float* ep = (float*)smem + wid * 16 * EP_LD;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ep[(fq * 4 + e) * EP_LD + j * 16 + fr] = acc[i][j][e];
+    __syncthreads();
+    for (int f = lane; f < 16 * F4_PER_ROW; f += 64) {
+      const int r = f / F4_PER_ROW, c4 = f % F4_PER_ROW;
+      const int m = m0 + wm * 128 + i * 16 + r;
+      if (m < a.M) {
+        const float4_t v = *(const float4_t*)(ep + r * EP_LD + c4 * 4);
+        epilogue_store4(a, m, n0 + wn * TN + c4 * 4, v);
+      }
+    }
+  }
+}
+
 // ============================================================== fp32 MFMA kernel
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
   constexpr int BM = 64, BN = 64, BK = 16, LDK = BK + 1;
@@ -301,7 +493,32 @@ int launch_bf16(GemmArgs a, hipStream_t s) {
   return AACLIP_OK;
 }
 
+int launch_bf16_4ph(GemmArgs a, hipStream_t s) {
+  if (a.N % 256) return AACLIP_ERR_ARG;
+  a.tiles_m = ceil_div(a.M, 256);
+  a.tiles_n = a.N / 256;
+  const size_t lds = 2 * 4 * 128 * 128;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)gemm_bf16_4ph_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return AACLIP_ERR_LAUNCH;
+    attr_set = true;
+  }
+  gemm_bf16_4ph_kernel<<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
+int g_gemm_variant = 0;  // tuning hook (aaclip_set_gemm_variant); 0 = default dispatch
+
 }  // namespace
+
+extern "C" int aaclip_set_gemm_variant(int variant) {
+  if (variant < 0 || variant > 4) return AACLIP_ERR_ARG;
+  g_gemm_variant = variant;
+  return AACLIP_OK;
+}
 
 extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, const void* A,
                            int64_t lda, const void* W, int64_t ldw, void* C, int64_t ldc,
@@ -326,7 +543,19 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
     AACLIP_REQUIRE(K % 64 == 0 && N % 128 == 0);
     // 256x256 tiles when they fill the chip; 256x128 otherwise (N = 768/1024 GEMMs)
     const long t256 = (long)ceil_div(M, 256) * (N / 256);
-    if (N % 256 == 0 && t256 >= 2 * 256) return launch_bf16<256, 256, 2, 4>(a, s);
+    const bool big = N % 256 == 0 && t256 >= 2 * 256;
+    switch (g_gemm_variant) {
+      case 1: return launch_bf16<256, 256, 2, 4>(a, s);                                  // 2-stage only
+      case 2: return N % 256 == 0 ? launch_bf16_4ph(a, s) : launch_bf16<256, 128, 4, 2>(a, s);  // 4-phase always
+      case 3: return launch_bf16<256, 128, 4, 2>(a, s);
+      case 4: return N % 256 == 0 ? launch_bf16<320, 256, 2, 4>(a, s) : launch_bf16<256, 128, 4, 2>(a, s);
+      default: break;
+    }
+    (void)big;
+    // M = B*577 tiles badly by 256 (18464 = 72.1 x 256 at B=32: 3.42 waves of 256x256
+    // tiles for N=3072, 1.14 for N=1024); 320-row tiles give 58 M-tiles -> 0.91 / 2.72 /
+    // 3.63 waves for N = 1024 / 3072 / 4096 (measured 1.1-1.4x faster on every block GEMM).
+    if (N % 256 == 0) return launch_bf16<320, 256, 2, 4>(a, s);
     return launch_bf16<256, 128, 4, 2>(a, s);
   }
   AACLIP_REQUIRE(K % 16 == 0 && N % 64 == 0);

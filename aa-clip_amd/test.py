@@ -120,8 +120,9 @@ def main(argv=None):
             text_embeddings = get_adapted_text_embedding(model if adapt_text else clip_model, args.dataset, device)
         df = DataFrame(columns=["class name", "pixel AUC", "pixel AP", "image AUC", "image AP"])
         for class_name, image_dataset in image_datasets.items():
+            workers = 0 if args.dataset == "synthetic" else 4
             loader = torch.utils.data.DataLoader(image_dataset, batch_size=args.batch_size, shuffle=False,
-                                                 num_workers=4, pin_memory=True)
+                                                 num_workers=workers, pin_memory=True)
             with torch.no_grad():
                 masks, labels, preds, preds_image, file_names = get_predictions(
                     model=model, class_text_embeddings=text_embeddings[class_name], test_loader=loader,

@@ -87,7 +87,7 @@ def time_launches(fn, reps, stream):
 
 
 def roofline_gemm(eng, ws, reps=20):
-    """Dominant kernel = bf16 MFMA GEMM <256x256> (QKV and c_fc launches).
+    """Dominant kernel = bf16 MFMA GEMM <320x256> (QKV and c_fc launches).
     Average HIP-event launch duration over the two shapes it runs at."""
     s = torch.cuda.current_stream()
     blk = eng.blocks[0]
@@ -108,7 +108,7 @@ def roofline_gemm(eng, ws, reps=20):
     block_flops = f_qkv + f_fc + 2.0 * R * WIDTH * WIDTH + 2.0 * R * 4 * WIDTH * WIDTH + f_at
     block_ms = t_qkv + t_fc + t_o + t_pr + t_at
     return {
-        "kernel": "gemm_bf16_kernel<256,256,2,4> (QKV + c_fc launches)",
+        "kernel": "gemm_bf16_kernel<320,256,2,4> (QKV + c_fc launches)",
         "bound": "mfma", "unit": "TFLOP/s", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS,
         "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
         "avg_launch_us": round(t_avg * 1e3, 2),
@@ -143,28 +143,50 @@ def roofline_map(eng, ws, T, reps=50):
             "blur_upsample_GBs": round(B * S * S * 4 / (t_bu * 1e-3) / 1e9, 1)}
 
 
-def cpu_baseline(n_images: int):
-    """The numpy oracle (fp32 restatement of the reference, pinned to its golden
-    vectors) on this host's cores: forward + 4-level map + image score."""
+def cpu_baseline_and_parity(n_images: int, dev, streams: int):
+    """CPU leg on rank 0: the numpy oracle (fp32 restatement of the reference,
+    pinned to its golden vectors) timed on this host's cores over a bounded
+    sample (forward + 4-level map + image score per image), and the same images
+    through the GPU path with the SAME synthetic weights -> map error and
+    pixel-AUROC parity (sklearn roc_auc_score over seeded anomaly masks)."""
     import numpy as np
+    from sklearn.metrics import roc_auc_score
 
     from oracle import aaclip_np as R
     from oracle import synth
     sd = synth.clip_state_dict(111)
     ia, _ = synth.adapter_state_dicts(111)
     x = synth.images(111, n_images, 336)
+    masks = synth.masks(111, n_images, 336)[:, 0]
     T = np.linalg.qr(np.random.default_rng(0).standard_normal((768, 2)))[0].astype(np.float32)
     R.visual_forward(sd, ia, x[:1])  # warm-up (BLAS threads, page-in)
     t0 = time.perf_counter()
+    ref_maps, ref_scores = [], []
     for i in range(n_images):
         seg, det = R.visual_forward(sd, ia, x[i:i + 1])
-        R.anomaly_map(seg, T, 336, "Industrial")
-        R.image_score(det, T)
+        ref_maps.append(R.anomaly_map(seg, T, 336, "Industrial"))
+        ref_scores.append(R.image_score(det, T))
     dt = time.perf_counter() - t0
+    ref_maps, ref_scores = np.concatenate(ref_maps), np.concatenate(ref_scores)
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": round(n_images / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"{n_images} synthetic 336px images, bs=1, fp32 numpy oracle (oracle/aaclip_np.py), "
-                      f"{dt:.1f} s", "threads_env": os.environ.get("OMP_NUM_THREADS")}
+    base = {"value": round(n_images / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"{n_images} synthetic 336px images, bs=1, fp32 numpy oracle of the reference "
+                      f"(oracle/aaclip_np.py) on {threads} host threads, {dt:.1f} s"}
+    vp = {k: torch.from_numpy(v).to(dev) for k, v in sd.items() if k.startswith("visual.")}
+    eng = VisualEngine(vp, {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}, dtype=torch.bfloat16)
+    m, s = eng.predict(torch.from_numpy(x).to(dev), torch.from_numpy(T).to(dev), "Industrial", streams=streams)
+    gpu_maps, gpu_scores = m.cpu().numpy(), s.cpu().numpy()
+    lab = masks.reshape(-1) > 0
+    auc_gpu = float(roc_auc_score(lab, gpu_maps.reshape(-1)))
+    auc_cpu = float(roc_auc_score(lab, ref_maps.reshape(-1)))
+    err = np.abs(gpu_maps - ref_maps)
+    parity = {"images": n_images, "pixel_auroc_gpu": round(auc_gpu, 6), "pixel_auroc_cpu_ref": round(auc_cpu, 6),
+              "pixel_auroc_abs_diff": abs(auc_gpu - auc_cpu), "map_max_abs_err": float(err.max()),
+              "map_within_1e-3_abs_1e-2_rel": bool((err <= 1e-3 + 1e-2 * np.abs(ref_maps)).all()),
+              "image_score_max_abs_err": float(np.abs(gpu_scores - ref_scores).max()),
+              "image_labels_equal": bool(np.array_equal(gpu_scores > 0.5, ref_scores > 0.5)),
+              "compute": "GPU bf16 MFMA path vs CPU fp32 oracle, same synthetic weights/images/masks"}
+    return base, parity
 
 
 def main():
@@ -174,8 +196,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
     ap.add_argument("--img-size", type=int, default=336)
-    ap.add_argument("--cpu-images", type=int, default=2, help="images for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-images", type=int, default=4, help="images for the CPU baseline + parity (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--streams", type=int, default=2, help="concurrent image chunks per GPU (HIP streams)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -197,7 +220,7 @@ def main():
     gathered = torch.empty(world * B, device=dev) if world > 1 else None
 
     def step():
-        maps, score = eng.predict(x, T, "Industrial")
+        maps, score = eng.predict(x, T, "Industrial", streams=args.streams)
         if world > 1:
             dist.all_gather_into_tensor(gathered, score)
         return maps
@@ -241,6 +264,7 @@ def main():
                                "Industrial blur, per-GPU batch of images",
                    "global_batch": B * world, "img_size": S, "per_gpu_batch": B,
                    "parallelism": f"image-sharded dp{world} (+RCCL all-gather of image scores)",
+                   "streams_per_gpu": args.streams,
                    "gflop_per_image": round(flops_per_image((S // 14) ** 2 + 1) / 1e9, 2)},
     }
     line["tflops_whole_path"] = round(flops_per_image((S // 14) ** 2 + 1) * images / elapsed / 1e12, 1)
@@ -248,7 +272,7 @@ def main():
         line["roofline"] = roofline_gemm(eng, ws)
         line["roofline_map"] = roofline_map(eng, ws, T)
     if rank == 0 and world == 1 and args.cpu_images > 0:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_images)
+        line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(args.cpu_images, dev, args.streams)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

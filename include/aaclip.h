@@ -66,6 +66,13 @@ int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K,
                 int row_group, int row_group_out, int row_offset, void* stream);
 
 /*
+ * Tuning hook: select the bf16 GEMM kernel family for benchmarking
+ * (0 = default dispatch, 1 = 2-stage 256x256, 2 = 4-phase 256x256 whenever
+ * N % 256 == 0, 3 = 2-stage 256x128). Process-global; not for production use.
+ */
+int aaclip_set_gemm_variant(int variant);
+
+/*
  * Multi-head attention core, softmax(q k^T / sqrt(d)) v per head, flash-style
  * (scores never materialised). qkv: [batch*seq, 3*heads*head_dim] packed
  * [q|k|v] exactly as nn.MultiheadAttention's in_proj output; out:

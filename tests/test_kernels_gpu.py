@@ -31,6 +31,27 @@ def test_gemm_bf16_plain(dev, M, N, K):
     assert err < 1e-3 * ref.abs().max().item() + 1e-4, err
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (2000, 256, 64)])
+def test_gemm_bf16_variants(dev, variant, M, N, K):
+    """Every bf16 kernel family (2-stage 256x256, 4-phase 256x256, 2-stage 256x128)."""
+    from aaclip import _lib
+    if variant in (1, 4) and N % 256:
+        pytest.skip("256x256 tile needs N % 256 == 0")
+    torch.manual_seed(M * 7 + N)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device=dev)
+    out = torch.empty(M, N, device=dev)
+    _lib.call("aaclip_set_gemm_variant", variant)
+    try:
+        ops.gemm(a, w, out, bias=bias)
+    finally:
+        _lib.call("aaclip_set_gemm_variant", 0)
+    ref = a.double() @ w.double().T + bias.double()
+    assert (out.double() - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
+
+
 def test_gemm_bf16_asymmetric_identity(dev):
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     M = N = K = 256

@@ -1,0 +1,88 @@
+"""Kernel micro-benchmark: times the per-block kernels of the C2 workload
+(B=32, 577 tokens) in isolation with HIP events (random bf16 operands).
+
+    python tools/kbench.py [--reps 20] [--only gemm|attn|rows]
+Used for A/B work on the kernels and as the command profiled by rocprofv3 --pmc.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "aa-clip_amd"))
+
+import torch  # noqa: E402
+
+from aaclip import ops  # noqa: E402
+
+
+def timeit(fn, reps):
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    fn()
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--variants", default="0", help="comma list of GEMM variants, A/B interleaved")
+    ap.add_argument("--rounds", type=int, default=1)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    B, n, W = args.batch, 577, 1024
+    R = B * n
+    g = torch.Generator(device=dev).manual_seed(0)
+    rnd = lambda *s, std=1.0: (torch.randn(*s, device=dev, generator=g) * std)  # noqa: E731
+    h = rnd(R, W).bfloat16()
+    x = rnd(R, W)
+    res = {}
+    if args.only in ("", "gemm"):
+        shapes = {"qkv": (3 * W, W, dict(bias=True)), "out": (W, W, dict(bias=True, resid=True)),
+                  "fc": (4 * W, W, dict(bias=True, gelu=True)), "proj": (W, 4 * W, dict(bias=True, resid=True)),
+                  "adapter": (W, W, dict(leaky=True))}
+        from aaclip import _lib
+        variants = [int(v) for v in args.variants.split(",")]
+        data = {}
+        for name, (N, K, kw) in shapes.items():
+            a = rnd(R, K).bfloat16()
+            w = rnd(N, K, std=K ** -0.5).bfloat16()
+            bias = rnd(N, std=0.02)
+            out = torch.empty(R, N, device=dev, dtype=torch.float32 if (kw.get("resid") or kw.get("leaky")) else torch.bfloat16)
+            data[name] = (N, K, kw, a, w, bias, out)
+        for rnd_i in range(args.rounds):
+            for v in variants:
+                _lib.call("aaclip_set_gemm_variant", v)
+                for name, (N, K, kw, a, w, bias, out) in data.items():
+                    f = lambda: ops.gemm(a, w, out, bias=bias if kw.get("bias") else None, gelu=kw.get("gelu", False),  # noqa: E731
+                                         leaky=kw.get("leaky", False), residual=out if kw.get("resid") else None)
+                    ms = timeit(f, args.reps)
+                    key = name if len(variants) == 1 else f"{name}/v{v}"
+                    prev = res.get(key)
+                    if prev is None or ms < prev[0]:
+                        res[key] = (ms, 2.0 * R * N * K / ms / 1e9)
+        _lib.call("aaclip_set_gemm_variant", 0)
+    if args.only in ("", "attn"):
+        qkv = rnd(R, 3 * W).bfloat16()
+        o = torch.empty(R, W, device=dev, dtype=torch.bfloat16)
+        ms = timeit(lambda: ops.attention(qkv, o, B, n, 16), args.reps)
+        res["attn"] = (ms, 4.0 * B * n * n * W / ms / 1e9)
+    if args.only in ("", "rows"):
+        lw, lb = rnd(W), rnd(W)
+        ms = timeit(lambda: ops.layernorm(x, lw, lb, h), args.reps)
+        res["layernorm"] = (ms, (R * W * 6) / ms / 1e6)
+    for k, (ms, rate) in res.items():
+        unit = "GB/s" if k == "layernorm" else "TFLOP/s"
+        print(f"{k:10s} {ms * 1e3:9.1f} us  {rate:8.1f} {unit}")
+
+
+if __name__ == "__main__":
+    main()
