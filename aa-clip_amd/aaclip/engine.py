@@ -14,7 +14,7 @@ Data layout in HBM (token-major "NLD", one row per token):
   xb     bf16 [B*(P+1), 1024]   bf16 copy of x written by the c_proj epilogue (adapter input)
   u      fp32 [B*(P+1), 1024]   LeakyReLU(adapter(x))
   tap_l  cdt  [B*P, 1024]       ln_post(x[:, 1:]) at each level
-  seg    cdt  [B*P, (L+1)*768]  seg_proj of level l in cols l*768.., det_proj in cols L*768..
+  seg    fp32 [B*P, (L+1)*768]  seg_proj of level l in cols l*768.., det_proj in cols L*768..
 cdt = compute dtype: bf16 (MFMA bf16, perf path) or fp32 (fp32 MFMA, parity mode).
 Weights are packed once: nn.Linear [N,K] layout kept (the GEMM is A.W^T);
 conv1 flattened to [1024, 640] (K padded 588 -> 640 with zeros).
@@ -115,9 +115,12 @@ class VisualEngine:
             attn=e(R, WIDTH), fc=e(R, 4 * WIDTH), u=e(R, WIDTH, dt=torch.float32),
             xb=e(R, WIDTH, dt=torch.bfloat16) if cdt == torch.bfloat16 else None,
             taps=[e(B * P, WIDTH) for _ in range(L)],
-            # all level projections + det in one [B*P, (L+1)*768] buffer: level l at
-            # columns l*768, det_proj at L*768 (one row stride for the map kernel)
-            segbuf=e(B * P, (L + 1) * EMBED),
+            # all level projections + det in one [B*P, (L+1)*768] fp32 buffer: level l at
+            # columns l*768, det_proj at L*768 (one row stride for the map kernel).
+            # fp32 even in bf16 mode: bf16 rounding of these final features moves a
+            # patch cosine by ~1e-4 (x100 in the map) — the largest single bf16
+            # term in the anomaly-map error budget, for ~15 us per batch of 32.
+            segbuf=e(B * P, (L + 1) * EMBED, dt=torch.float32),
             grid=e(B * P, dt=torch.float32), partial=e(B * ((P + 63) // 64) * EMBED, dt=torch.float32),
             det=e(B, EMBED, dt=torch.float32), score=e(B, dt=torch.float32),
             map=e(B, S, S, dt=torch.float32),

@@ -34,19 +34,146 @@ __device__ __forceinline__ short4_t tr_read(const char* p) {
 // byte offset of (row, 16-B chunk) in a swizzled [64][128 B] tile
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
-__global__ __launch_bounds__(256) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
+// Cross-lane max over the 4 lanes {c, c+16, c+32, c+48} that hold one query's
+// scores: v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip).
+__device__ __forceinline__ float max_over_groups(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float sum_over_groups(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// One 64-key tile for one wave: NKB live 16-key blocks (1, 2 or 4), NQB live
+// 16-query blocks (1 or 2), MASK = tile needs the key-tail / causal mask.
+// Dead blocks and the mask are resolved at compile time, so the 577 = 9*64 + 1
+// key tail costs 1/4 of a tile and full tiles carry no masking code.
+// Scores stay unscaled until the exponent: max on raw S (the scale is > 0),
+// p = exp2(S * log2e/8 - m2) as one FMA + one v_exp_f32. The O rescale is
+// skipped when no row max in the wave moved (alpha == 1 everywhere).
+template <int NKB, int NQB, bool MASK>
+__device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&qf)[2][2], float4_t (&ot)[2][4],
+                                          float (&m_run)[2], float (&l_run)[2], int key0, int q0, int N,
+                                          int causal, int g, int c) {
+  constexpr float sl2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+  const char* vt_lds = kt_lds + KT * 128;
+  float4_t st[NQB][NKB];
+#pragma unroll
+  for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) st[qb][kb] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t kf = *(const bf16x8_t*)(kt_lds + swz(kb * 16 + c, ks * 4 + g));
+#pragma unroll
+      for (int qb = 0; qb < NQB; ++qb)
+        st[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qb][ks], st[qb][kb], 0, 0, 0);
+    }
+  }
+  constexpr int NKS = (NKB + 1) / 2;  // 32-key MFMA steps for P.V
+  bf16x8_t pf[NQB][NKS];
+#pragma unroll
+  for (int qb = 0; qb < NQB; ++qb) {
+    float mx = -INFINITY;
+    if constexpr (MASK) {
+      // keys valid for this lane's query: key < lim
+      const int q = q0 + qb * 16 + c;
+      const int lim = (causal ? min(N, q + 1) : N) - key0 - 4 * g;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float sv = (kb * 16 + i < lim) ? st[qb][kb][i] : -INFINITY;
+          st[qb][kb][i] = sv;
+          mx = fmaxf(mx, sv);
+        }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[qb][kb][i]);
+    }
+    mx = max_over_groups(mx);
+    const float m_old = m_run[qb];
+    const float m_new = fmaxf(m_old, mx * sl2);
+    m_run[qb] = m_new;
+    float ls = 0.f;
+    float p[2 * NKS][4];
+#pragma unroll
+    for (int kb = 0; kb < 2 * NKS; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        p[kb][i] = kb < NKB ? __builtin_amdgcn_exp2f(fmaf(st[qb][kb < NKB ? kb : 0][i], sl2, -m_new)) : 0.f;
+        ls += p[kb][i];
+      }
+    if (__builtin_amdgcn_ballot_w64(m_new != m_old) != 0) {  // wave-uniform
+      const float alpha = __builtin_amdgcn_exp2f(m_old - m_new);
+      l_run[qb] *= alpha;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ot[qb][db][e] *= alpha;
+    }
+    l_run[qb] += ls;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      bf16x8_t v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = (__bf16)p[2 * ks][i];
+        v[4 + i] = (__bf16)p[2 * ks + 1][i];
+      }
+      pf[qb][ks] = v;
+    }
+  }
+  // O^T += V^T . P^T ; V^T fragment via transposing LDS reads
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int qq = c >> 2, pp = c & 3;
+      const int chunk = db * 2 + (pp >> 1);
+      const int r0 = ks * 32 + 4 * g + qq;
+      const short4_t lo = tr_read(vt_lds + swz(r0, chunk) + (pp & 1) * 8);
+      const short4_t hi = tr_read(vt_lds + swz(r0 + 16, chunk) + (pp & 1) * 8);
+      const short8_t vv = short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, vv);
+#pragma unroll
+      for (int qb = 0; qb < NQB; ++qb)
+        ot[qb][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb][ks], ot[qb][db], 0, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
                                                         uint16_t* __restrict__ out, int N, int H,
                                                         int causal) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * KT * 128];  // [stage][K|V][64][128B]
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, c = lane & 15;
-  const int bh = blockIdx.y;
+  // XCD-aware remap of the 1-D grid: blocks b, b+8, ... share an XCD (its L2), so
+  // give each XCD a contiguous run of work ids and order work ids query-tile
+  // fastest: all query tiles of one (image, head) then read that head's K/V from
+  // the same L2 instead of from 5 different XCDs (PMC: L2 hit rate 20% before).
+  const int nq = (N + QT - 1) / QT;
+  const int nwg = gridDim.x;
+  const int xcd = blockIdx.x & 7, qd = nwg >> 3, rd = nwg & 7;
+  const int wgid = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (blockIdx.x >> 3);
+  const int qtile = wgid % nq;
+  const int bh = wgid / nq;
   const int b = bh / H, h = bh % H;
   const int HDt = H * HD_;
   const int64_t ld = 3 * (int64_t)HDt;
   const uint16_t* base = qkv + (size_t)b * N * ld + h * HD_;
-  const int q0 = blockIdx.x * QT + wid * QW;
+  const int q0 = qtile * QT + wid * QW;
 
   // ---- Q fragments (B operand of K.Q^T): lane holds Q[q][ks*32 + 8g .. +7]
   bf16x8_t qf[2][2];
@@ -89,117 +216,47 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(const uint16_t* __restri
     for (int db = 0; db < 4; ++db) ot[qb][db] = float4_t{0.f, 0.f, 0.f, 0.f};
   float m_run[2] = {-INFINITY, -INFINITY};
   float l_run[2] = {0.f, 0.f};  // per-lane partial row sums (reduced over g at the end)
-  const float sl2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
 
   int ntiles = (N + KT - 1) / KT;
   if (causal) {
-    const int last_q = min(blockIdx.x * QT + QT - 1, N - 1);
+    const int last_q = min(qtile * QT + QT - 1, N - 1);
     ntiles = min(ntiles, last_q / KT + 1);
   }
 
   stage(0, 0);
   __syncthreads();
+  // wave-uniform work shape: query blocks with any valid row, key blocks of the tile
+  const int nqb = q0 + 16 < N ? 2 : (q0 < N ? 1 : 0);
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     if (t + 1 < ntiles) stage(t + 1, cur ^ 1);
     const char* kt_lds = smem + cur * (2 * KT * 128);
-    const char* vt_lds = kt_lds + KT * 128;
-
-    // ---- S^T = K . Q^T : st[qb][kb][i] = S[q = qb*16+c][key = kb*16 + 4g + i]
-    float4_t st[2][4];
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) st[qb][kb] = float4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t kf = *(const bf16x8_t*)(kt_lds + swz(kb * 16 + c, ks * 4 + g));
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-          st[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qb][ks], st[qb][kb], 0, 0, 0);
-      }
-    }
-
-    // ---- online softmax (log2 domain)
     const int key0 = t * KT;
-    const bool tail = (key0 + KT > N) || causal;
-    bf16x8_t pf[2][2];
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int q = q0 + qb * 16 + c;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float s = st[qb][kb][i] * sl2;
-          if (tail) {
-            const int key = key0 + kb * 16 + 4 * g + i;
-            if (key >= N || (causal && key > q)) s = -INFINITY;
-          }
-          st[qb][kb][i] = s;
-          mx = fmaxf(mx, s);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run[qb], mx);
-      const float alpha = __builtin_amdgcn_exp2f(m_run[qb] - m_new);
-      m_run[qb] = m_new;
-      float ls = 0.f;
-      float p[4][4];
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          p[kb][i] = __builtin_amdgcn_exp2f(st[qb][kb][i] - m_new);
-          ls += p[kb][i];
-        }
-      l_run[qb] = l_run[qb] * alpha + ls;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) ot[qb][db] *= alpha;
-      // P^T as the B operand: k-step ks holds keys {32ks+4g+i} (j<4) and {32ks+16+4g+i} (j>=4)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = (__bf16)p[2 * ks][i];
-          v[4 + i] = (__bf16)p[2 * ks + 1][i];
-        }
-        pf[qb][ks] = v;
-      }
+    const int live = min(KT, N - key0);               // valid keys in this tile
+    const bool masked = (live < KT) || (causal && key0 + KT - 1 > q0);
+    const int nkb = live > 32 ? 4 : (live > 16 ? 2 : 1);  // 16-key blocks to compute
+#define ATTN_TILE(NKB_, NQB_, M_) \
+    attn_tile<NKB_, NQB_, M_>(kt_lds, qf, ot, m_run, l_run, key0, q0, N, causal, g, c)
+    if (!masked) {
+      if (nqb == 2) ATTN_TILE(4, 2, false);
+      else if (nqb == 1) ATTN_TILE(4, 1, false);
+    } else if (nqb == 2) {
+      if (nkb == 4) ATTN_TILE(4, 2, true);
+      else if (nkb == 2) ATTN_TILE(2, 2, true);
+      else ATTN_TILE(1, 2, true);
+    } else if (nqb == 1) {
+      if (nkb == 4) ATTN_TILE(4, 1, true);
+      else if (nkb == 2) ATTN_TILE(2, 1, true);
+      else ATTN_TILE(1, 1, true);
     }
-
-    // ---- O^T += V^T . P^T ; V^T fragment via transposing LDS reads
-#pragma unroll
-    for (int db = 0; db < 4; ++db) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        // lane 4q+p of the 16-lane group addresses row (key) 32ks + [16] + 4g + q,
-        // columns d = db*16 + 4p .. +3
-        const int qq = c >> 2, pp = c & 3;
-        const int chunk = db * 2 + (pp >> 1);
-        const int r0 = ks * 32 + 4 * g + qq;
-        const short4_t lo = tr_read(vt_lds + swz(r0, chunk) + (pp & 1) * 8);
-        const short4_t hi = tr_read(vt_lds + swz(r0 + 16, chunk) + (pp & 1) * 8);
-        const short8_t vv = short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, vv);
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-          ot[qb][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb][ks], ot[qb][db], 0, 0, 0);
-      }
-    }
+#undef ATTN_TILE
     __syncthreads();
   }
 
   // ---- epilogue: O[q][d = db*16 + 4g + i] = ot / l
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    float l = l_run[qb];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    const float l = sum_over_groups(l_run[qb]);
     const float inv = 1.0f / l;
     const int q = q0 + qb * 16 + c;
     if (q < N) {
@@ -290,8 +347,9 @@ extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch
   AACLIP_REQUIRE(qkv && out && batch > 0 && seq > 0 && heads > 0 && head_dim == HD_);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == AACLIP_BF16) {
-    dim3 grid(ceil_div(seq, QT), batch * heads);
-    attn_bf16_kernel<<<grid, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, seq, heads, causal);
+    const long nwg = (long)ceil_div(seq, QT) * batch * heads;
+    AACLIP_REQUIRE(nwg < (1L << 31));
+    attn_bf16_kernel<<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, seq, heads, causal);
   } else {
     dim3 grid(ceil_div(seq, 64), batch * heads);
     attn_f32_kernel<<<grid, 64, 0, s>>>((const float*)qkv, (float*)out, seq, heads, causal);

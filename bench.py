@@ -122,14 +122,14 @@ def roofline_gemm(eng, ws, reps=20):
 
 
 def roofline_map(eng, ws, T, reps=50):
-    """Anomaly-map stream kernel (patch_scores): algorithmic bytes = L*P*768*2 (bf16
-    features) + 768*2*4 (anchors) + P*4 (score grid) per image."""
+    """Anomaly-map stream kernel (patch_scores): algorithmic bytes = L*P*768*4 (fp32
+    level features) + 768*2*4 (anchors) + P*4 (score grid) per image."""
     s = torch.cuda.current_stream()
     L = ws["segbuf"].shape[1] // 768 - 1
     seg = [ws["segbuf"][:, j * 768:(j + 1) * 768] for j in range(L)]
     rows = seg[0].shape[0]
     t_ps = time_launches(lambda: ops.patch_scores(seg, T, ws["grid"]), reps, s)
-    nbytes = len(seg) * rows * 768 * 2 + 768 * 2 * 4 + rows * 4
+    nbytes = len(seg) * rows * 768 * seg[0].element_size() + 768 * 2 * 4 + rows * 4
     B = rows // ws["P"]
     S = ws["map"].shape[-1]
     g = ws["g"]
@@ -173,19 +173,26 @@ def cpu_baseline_and_parity(n_images: int, dev, streams: int):
             "sample": f"{n_images} synthetic 336px images, bs=1, fp32 numpy oracle of the reference "
                       f"(oracle/aaclip_np.py) on {threads} host threads, {dt:.1f} s"}
     vp = {k: torch.from_numpy(v).to(dev) for k, v in sd.items() if k.startswith("visual.")}
-    eng = VisualEngine(vp, {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}, dtype=torch.bfloat16)
-    m, s = eng.predict(torch.from_numpy(x).to(dev), torch.from_numpy(T).to(dev), "Industrial", streams=streams)
-    gpu_maps, gpu_scores = m.cpu().numpy(), s.cpu().numpy()
+    iad = {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}
     lab = masks.reshape(-1) > 0
-    auc_gpu = float(roc_auc_score(lab, gpu_maps.reshape(-1)))
     auc_cpu = float(roc_auc_score(lab, ref_maps.reshape(-1)))
-    err = np.abs(gpu_maps - ref_maps)
-    parity = {"images": n_images, "pixel_auroc_gpu": round(auc_gpu, 6), "pixel_auroc_cpu_ref": round(auc_cpu, 6),
-              "pixel_auroc_abs_diff": abs(auc_gpu - auc_cpu), "map_max_abs_err": float(err.max()),
-              "map_within_1e-3_abs_1e-2_rel": bool((err <= 1e-3 + 1e-2 * np.abs(ref_maps)).all()),
-              "image_score_max_abs_err": float(np.abs(gpu_scores - ref_scores).max()),
-              "image_labels_equal": bool(np.array_equal(gpu_scores > 0.5, ref_scores > 0.5)),
-              "compute": "GPU bf16 MFMA path vs CPU fp32 oracle, same synthetic weights/images/masks"}
+    tol = 1e-3 + 1e-2 * np.abs(ref_maps)
+    parity = {"images": n_images, "pixel_auroc_cpu_ref": round(auc_cpu, 6),
+              "tolerance": "maps |gpu - ref| <= 1e-3 + 1e-2*|ref| (north_star)",
+              "reference": "CPU fp32 numpy oracle (pinned to the reference's golden vectors), same "
+                           "synthetic weights/images/masks"}
+    for tag, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+        eng = VisualEngine(vp, iad, dtype=dt)
+        m, s = eng.predict(torch.from_numpy(x).to(dev), torch.from_numpy(T).to(dev), "Industrial", streams=streams)
+        gpu_maps, gpu_scores = m.cpu().numpy(), s.cpu().numpy()
+        err = np.abs(gpu_maps - ref_maps)
+        auc_gpu = float(roc_auc_score(lab, gpu_maps.reshape(-1)))
+        parity[tag] = {"pixel_auroc_gpu": round(auc_gpu, 6), "pixel_auroc_abs_diff": abs(auc_gpu - auc_cpu),
+                       "map_max_abs_err": float(err.max()), "map_within_tol": bool((err <= tol).all()),
+                       "frac_pixels_within_tol": float((err <= tol).mean()),
+                       "image_score_max_abs_err": float(np.abs(gpu_scores - ref_scores).max()),
+                       "image_labels_equal": bool(np.array_equal(gpu_scores > 0.5, ref_scores > 0.5))}
+        del eng
     return base, parity
 
 
