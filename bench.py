@@ -35,6 +35,18 @@ from aaclip import ops  # noqa: E402
 from aaclip.engine import HEADS, LAYERS, WIDTH, VisualEngine  # noqa: E402
 
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(key):
+    """HBM bytes per launch measured by rocprofv3 PMC passes on the same kernels
+    and shapes (profiles/pmc_traffic.json, written by tools/pmc_summary.py)."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+        return t[key]["bytes_per_launch"], t["source"]
+    except (OSError, KeyError, ValueError):
+        return None, None
 HBM_PEAK_GBS = 8000.0      # HBM3E spec peak
 
 
@@ -107,10 +119,13 @@ def roofline_gemm(eng, ws, reps=20):
     f_at = 4.0 * B * n * n * WIDTH
     block_flops = f_qkv + f_fc + 2.0 * R * WIDTH * WIDTH + 2.0 * R * 4 * WIDTH * WIDTH + f_at
     block_ms = t_qkv + t_fc + t_o + t_pr + t_at
+    traffic, src = pmc_traffic("gemm")
     return {
         "kernel": "gemm_bf16_kernel<320,256,2,4> (QKV + c_fc launches)",
         "bound": "mfma", "unit": "TFLOP/s", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS,
-        "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+        "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_source": src,
+        "algorithmic_bytes_per_launch": (R * WIDTH * 2 + 3 * WIDTH * WIDTH * 2 + R * 3 * WIDTH * 2
+                                         + R * WIDTH * 2 + 4 * WIDTH * WIDTH * 2 + R * 4 * WIDTH * 2) / 2,
         "avg_launch_us": round(t_avg * 1e3, 2),
         "flops_per_launch": (f_qkv + f_fc) / 2,
         "attn_mlp_block": {"tflops": round(block_flops / (block_ms * 1e-3) / 1e12, 1),
@@ -136,8 +151,9 @@ def roofline_map(eng, ws, T, reps=50):
     t_bu = time_launches(lambda: ops.blur_upsample(ws["grid"].view(B, 1, g, g), ws["map"].view(B, 1, S, S),
                                                    ksize=7, sigma=1.0), reps, s)
     gbs = nbytes / (t_ps * 1e-3) / 1e9
+    traffic, src = pmc_traffic("map")
     return {"kernel": "patch_scores_kernel", "bound": "hbm", "unit": "GB/s", "achieved": round(gbs, 1),
-            "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
             "avg_launch_us": round(t_ps * 1e3, 2), "bytes_per_launch": nbytes,
             "blur_upsample_us": round(t_bu * 1e3, 2),
             "blur_upsample_GBs": round(B * S * S * 4 / (t_bu * 1e-3) / 1e9, 1)}

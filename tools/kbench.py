@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--variants", default="0", help="comma list of GEMM variants, A/B interleaved")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--shapes", default="qkv,out,fc,proj,adapter", help="GEMM shapes to run")
+    ap.add_argument("--map", action="store_true", help="also run the anomaly-map stream kernel (C2 sizes)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, n, W = args.batch, 577, 1024
@@ -52,6 +54,7 @@ def main():
         from aaclip import _lib
         variants = [int(v) for v in args.variants.split(",")]
         data = {}
+        shapes = {n: v for n, v in shapes.items() if n in args.shapes.split(",")}
         for name, (N, K, kw) in shapes.items():
             a = rnd(R, K).bfloat16()
             w = rnd(N, K, std=K ** -0.5).bfloat16()
@@ -75,12 +78,20 @@ def main():
         o = torch.empty(R, W, device=dev, dtype=torch.bfloat16)
         ms = timeit(lambda: ops.attention(qkv, o, B, n, 16), args.reps)
         res["attn"] = (ms, 4.0 * B * n * n * W / ms / 1e9)
+    if args.map:
+        P = B * 576
+        seg = rnd(P, 5 * 768)
+        levels = [seg[:, j * 768:(j + 1) * 768] for j in range(4)]
+        T = torch.nn.functional.normalize(rnd(768, 2), dim=0).contiguous()
+        grid = torch.empty(P, device=dev)
+        ms = timeit(lambda: ops.patch_scores(levels, T, grid), args.reps)
+        res["patch_scores"] = (ms, (4 * P * 768 * 4 + P * 4) / ms / 1e6)
     if args.only in ("", "rows"):
         lw, lb = rnd(W), rnd(W)
         ms = timeit(lambda: ops.layernorm(x, lw, lb, h), args.reps)
         res["layernorm"] = (ms, (R * W * 6) / ms / 1e6)
     for k, (ms, rate) in res.items():
-        unit = "GB/s" if k == "layernorm" else "TFLOP/s"
+        unit = "GB/s" if k in ("layernorm", "patch_scores") else "TFLOP/s"
         print(f"{k:10s} {ms * 1e3:9.1f} us  {rate:8.1f} {unit}")
 
 
