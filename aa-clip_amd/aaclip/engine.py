@@ -220,9 +220,10 @@ class VisualEngine:
         x = x.to(self.device, torch.float32).contiguous()
         bounds = [(B * i) // streams for i in range(streams + 1)]
         main = torch.cuda.current_stream(self.device)
-        ready = torch.cuda.Event()
+        if len(getattr(self, "_events", [])) < streams + 1:
+            self._events = [torch.cuda.Event() for _ in range(streams + 1)]
+        ready, done = self._events[0], self._events[1:streams + 1]
         ready.record(main)
-        done = []
         for i, st in enumerate(self._chunk_streams(streams)):
             b0, b1 = bounds[i], bounds[i + 1]
             with torch.cuda.stream(st):
@@ -231,12 +232,39 @@ class VisualEngine:
                 ops.anomaly_map(seg_raw, T, out_map[b0:b1], ws["grid"], g=ws["g"], ksize=k, sigma=s)
                 ops.image_score(det_raw, b1 - b0, ws["P"], ws["partial"], det=ws["det"], T=T,
                                 score=out_score[b0:b1])
-                ev = torch.cuda.Event()
-                ev.record(st)
-                done.append(ev)
+                done[i].record(st)
         for ev in done:
             main.wait_event(ev)
         return out_map, out_score
+
+    @torch.no_grad()
+    def graphed_predict(self, batch: int, img_size: int, domain: str = "Industrial", streams: int = 1):
+        """Capture predict() for a fixed (batch, size, domain, streams) into one hipGraph
+        (torch.cuda.CUDAGraph records the C-ABI launches on the capturing stream and the
+        chunk streams' fork/join). Returns fn(x, T) -> (map, score) that copies the
+        inputs into static device buffers and replays the graph: no per-kernel host
+        launch cost (matters at small batch, e.g. config C1's bs=1)."""
+        x_s = torch.zeros(batch, 3, img_size, img_size, device=self.device)
+        T_s = torch.zeros(EMBED, 2, device=self.device)
+        T_s[0, 0] = 1.0
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):  # warm-up: allocate workspaces, set kernel attributes
+            self.predict(x_s, T_s, domain, streams=streams)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out_map, out_score = self.predict(x_s, T_s, domain, streams=streams)
+
+        def run(x: torch.Tensor, T: torch.Tensor):
+            x_s.copy_(x, non_blocking=True)
+            T_s.copy_(T, non_blocking=True)
+            graph.replay()
+            return out_map, out_score
+
+        run.graph = graph
+        return run
 
 
 class TextEngine:

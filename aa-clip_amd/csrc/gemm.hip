@@ -37,6 +37,9 @@ struct GemmArgs {
   int epi, out_dtype;
   int row_group, row_group_out, row_offset;
   int tiles_m, tiles_n;
+  int group_m;   // tile-order group height (L2 reuse), default 8
+  int setprio;   // raise wave priority around the MFMA cluster
+  int dbg;       // diagnostic: 1 = skip the epilogue (accumulators kept live)
 };
 
 __device__ __forceinline__ int remap_row(const GemmArgs& a, int m) {
@@ -101,12 +104,12 @@ __device__ __forceinline__ void epilogue_store4(const GemmArgs& a, int m, int n,
 }
 
 // Bijective XCD remap (blocks b, b+8, ... share an XCD) + grouped tile order.
-__device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+__device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, int& tm, int& tn,
+                                            int GROUP_M = 8) {
   const int nwg = tiles_m * tiles_n;
   const int xcd = bid & 7;
   const int q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  constexpr int GROUP_M = 8;
   const int per_group = GROUP_M * tiles_n;
   const int group = wgid / per_group;
   const int first_m = group * GROUP_M;
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   const int wm = wid / WN, wn = wid % WN;
 
   int tm, tn;
-  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn);
+  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const uint16_t* __restrict__ Ag = (const uint16_t*)a.A;
@@ -203,6 +206,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
     const int cur = kt & 1;
     if (kt + 1 < nk) GEMM_STAGE(kt + 1, cur ^ 1);
     const char* base = smem + cur * STAGE_BYTES;
+    if (a.setprio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8_t bf[RN];
@@ -216,23 +220,34 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (a.setprio) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
   }
 
   // ---- epilogue, staged through LDS one 16-row block at a time so that each lane
   // finishes 4 consecutive columns (16-B fp32 / 8-B bf16 stores, coalesced rows).
-  // Accumulator layout: lane holds C[16i + 4*fq + e][16j + fr].
+  // Accumulator layout: lane holds C[16i + 4*fq + e][16j + fr]. Each wave stages
+  // through its own LDS slot (the main loop's last barrier freed the tiles), so
+  // no workgroup barrier is needed: LDS ops of one wave execute in order, and the
+  // asm memory fences keep the compiler from reordering the write/read phases.
   constexpr int EP_LD = TN + 4;  // floats per staged row (pad: conflict-free writes)
   float* ep = (float*)smem + wid * 16 * EP_LD;
   constexpr int F4_PER_ROW = TN / 4;
+  if (a.dbg & 1) {  // diagnostic timing build path: keep the MFMA results live, store nothing
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
-    __syncthreads();
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int j = 0; j < RN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) ep[(fq * 4 + e) * EP_LD + j * 16 + fr] = acc[i][j][e];
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (int f = lane; f < 16 * F4_PER_ROW; f += 64) {
       const int r = f / F4_PER_ROW, c4 = f % F4_PER_ROW;
       const int m = m0 + wm * TM + i * 16 + r;
@@ -242,6 +257,169 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
       }
     }
   }
+}
+
+// ============================================================== bf16 MFMA, persistent
+// Same tile / main loop as gemm_bf16_kernel, but each workgroup loops over the
+// tiles L = blockIdx.x, blockIdx.x + gridDim.x, ... (gridDim.x = #CUs; the
+// linear id keeps the XCD-aware order of tile_coords). Tile seams are
+// pipelined: during the last K-step of tile i the DMA of tile i+1's first
+// K-stage is issued into the free buffer; tile i's epilogue stages through the
+// buffer just consumed; tile i+1's first barrier waits with vmcnt(NSTORE), not 0.
+// vmcnt retires in issue order and the prefetch is older than the epilogue's
+// stores, so the wait guarantees the prefetch landed while up to NSTORE of the
+// previous tile's output stores keep draining behind the next main loop.
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_persistent_kernel(GemmArgs a) {
+  constexpr int NWAVES = WM * WN;
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int RM = TM / 16, RN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int A_LOADS = A_BYTES / (NWAVES * 1024);
+  constexpr int B_LOADS = B_BYTES / (NWAVES * 1024);
+  constexpr int EP_LD = TN + 4, F4_PER_ROW = TN / 4;
+  constexpr int STORES_PER_WAVE = RM * (16 * F4_PER_ROW / 64);  // C stores per wave per tile
+  static_assert(A_LOADS * NWAVES * 1024 == A_BYTES && B_LOADS * NWAVES * 1024 == B_BYTES, "tile");
+  static_assert((16 * F4_PER_ROW) % 64 == 0, "epilogue store count must be lane-uniform");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ntiles = a.tiles_m * a.tiles_n;
+  const int nk = a.K / BK;
+  const uint16_t* __restrict__ Ag = (const uint16_t*)a.A;
+  const uint16_t* __restrict__ Wg = (const uint16_t*)a.W;
+
+  const uint16_t* a_src[A_LOADS];
+  const uint16_t* b_src[B_LOADS];
+  auto set_sources = [&](int m0_, int n0_) {
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      const int r = (i * NWAVES + wid) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      a_src[i] = Ag + (size_t)min(m0_ + r, a.M - 1) * a.lda + c * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      const int r = (i * NWAVES + wid) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      b_src[i] = Wg + (size_t)(n0_ + r) * a.ldw + c * 8;
+    }
+  };
+#define PGEMM_STAGE(kt, buf)                                                                   \
+  do {                                                                                         \
+    char* base_ = smem + (buf) * STAGE_BYTES;                                                  \
+    const int koff_ = (kt) * BK;                                                               \
+    _Pragma("unroll") for (int i = 0; i < A_LOADS; ++i)                                        \
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + koff_),                        \
+                                       LDS_PTR(base_ + (i * NWAVES + wid) * 1024), 16, 0, 0);   \
+    _Pragma("unroll") for (int i = 0; i < B_LOADS; ++i)                                        \
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + koff_),                        \
+                                       LDS_PTR(base_ + A_BYTES + (i * NWAVES + wid) * 1024),   \
+                                       16, 0, 0);                                              \
+  } while (0)
+
+  int a_off[RM][2], b_off[RN][2];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int r = wm * TM + i * 16 + fr;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) a_off[i][kk] = r * 128 + (((kk * 4 + fq) ^ (r & 7)) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int r = wn * TN + j * 16 + fr;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) b_off[j][kk] = A_BYTES + r * 128 + (((kk * 4 + fq) ^ (r & 7)) << 4);
+  }
+
+  int L = blockIdx.x;
+  if (L >= ntiles) return;
+  int tm, tn;
+  tile_coords(L, a.tiles_m, a.tiles_n, tm, tn);
+  set_sources(tm * BM, tn * BN);
+  int it = 0;  // running K-step counter: buffer parity continues across tiles
+  PGEMM_STAGE(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  bool pending_stores = false;
+
+  while (true) {
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int Ln = L + gridDim.x;
+    const bool has_next = Ln < ntiles;
+    int tm_n = 0, tn_n = 0;
+    if (has_next) tile_coords(Ln, a.tiles_m, a.tiles_n, tm_n, tn_n);
+    if (pending_stores) {
+      // the previous tile's prefetch (older) must have landed; its stores may drain
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(STORES_PER_WAVE < 63 ? STORES_PER_WAVE : 63)
+                   : "memory");
+    }
+    float4_t acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt, ++it) {
+      const int cur = it & 1;
+      if (kt + 1 < nk) {
+        PGEMM_STAGE(kt + 1, cur ^ 1);
+      } else if (has_next) {
+        set_sources(tm_n * BM, tn_n * BN);  // current tile's DMA all issued: retarget
+        PGEMM_STAGE(0, cur ^ 1);
+      }
+      const char* base = smem + cur * STAGE_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8_t bf[RN];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bf[j] = *(const bf16x8_t*)(base + b_off[j][kk]);
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+          const bf16x8_t af = *(const bf16x8_t*)(base + a_off[i][kk]);
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
+        }
+      }
+      if (kt + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      else  // all reads of `cur` done before it becomes the epilogue staging area
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // ---- epilogue through the just-consumed buffer (the other one is loading)
+    float* ep = (float*)(smem + ((it - 1) & 1) * STAGE_BYTES) + wid * 16 * EP_LD;
+    const bool full_tile = m0 + BM <= a.M;
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ep[(fq * 4 + e) * EP_LD + j * 16 + fr] = acc[i][j][e];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int f = lane; f < 16 * F4_PER_ROW; f += 64) {
+        const int r = f / F4_PER_ROW, c4 = f % F4_PER_ROW;
+        const int m = m0 + wm * TM + i * 16 + r;
+        if (full_tile || m < a.M) {
+          const float4_t v = *(const float4_t*)(ep + r * EP_LD + c4 * 4);
+          epilogue_store4(a, m, n0 + wn * TN + c4 * 4, v);
+        }
+      }
+    }
+    if (!has_next) break;
+    // a partial tile issued fewer stores than the counted wait assumes: drain fully
+    if (!full_tile) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // epilogue LDS reads done before the barrier
+    pending_stores = true;
+    L = Ln;
+    tm = tm_n;
+    tn = tn_n;
+  }
+#undef PGEMM_STAGE
 }
 
 // ============================================================== bf16 MFMA, 4-phase pipeline
@@ -510,13 +688,52 @@ int launch_bf16_4ph(GemmArgs a, hipStream_t s) {
   return AACLIP_OK;
 }
 
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_bf16_persistent(GemmArgs a, hipStream_t s) {
+  if (a.N % BN) return AACLIP_ERR_ARG;
+  a.tiles_m = ceil_div(a.M, BM);
+  a.tiles_n = a.N / BN;
+  const int ntiles = a.tiles_m * a.tiles_n;
+  const size_t lds = 2 * (size_t)(BM + BN) * 64 * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)gemm_bf16_persistent_kernel<BM, BN, WM, WN>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return AACLIP_ERR_LAUNCH;
+    attr_set = true;
+  }
+  const int grid = min(ntiles, num_cus());
+  gemm_bf16_persistent_kernel<BM, BN, WM, WN><<<grid, WM * WN * 64, lds, s>>>(a);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
 int g_gemm_variant = 0;  // tuning hook (aaclip_set_gemm_variant); 0 = default dispatch
+int g_group_m = 8;
+int g_setprio = 0;
+int g_dbg = 0;
 
 }  // namespace
 
 extern "C" int aaclip_set_gemm_variant(int variant) {
-  if (variant < 0 || variant > 4) return AACLIP_ERR_ARG;
-  g_gemm_variant = variant;
+  // bits 0-3: kernel family; bits 4-7: tile-order group height (0 = 8); bit 8: setprio
+  const int fam = variant & 15, grp = (variant >> 4) & 15;
+  if (variant < 0 || fam > 5) return AACLIP_ERR_ARG;
+  g_gemm_variant = fam;
+  g_group_m = grp ? grp : 8;
+  g_setprio = (variant >> 8) & 1;
+  g_dbg = (variant >> 9) & 1;
   return AACLIP_OK;
 }
 
@@ -537,7 +754,7 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
   AACLIP_REQUIRE(row_group >= 0 && (row_group == 0 || row_group_out >= row_group));
   if (M == 0) return AACLIP_OK;
   GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
-             out_dtype, row_group, row_group_out, row_offset, 0, 0};
+             out_dtype, row_group, row_group_out, row_offset, 0, 0, g_group_m, g_setprio, g_dbg};
   hipStream_t s = (hipStream_t)stream;
   if (in_dtype == AACLIP_BF16) {
     AACLIP_REQUIRE(K % 64 == 0 && N % 128 == 0);
@@ -549,6 +766,7 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
       case 2: return N % 256 == 0 ? launch_bf16_4ph(a, s) : launch_bf16<256, 128, 4, 2>(a, s);  // 4-phase always
       case 3: return launch_bf16<256, 128, 4, 2>(a, s);
       case 4: return N % 256 == 0 ? launch_bf16<320, 256, 2, 4>(a, s) : launch_bf16<256, 128, 4, 2>(a, s);
+      case 5: return N % 256 == 0 ? launch_bf16_persistent<320, 256, 2, 4>(a, s) : launch_bf16<256, 128, 4, 2>(a, s);
       default: break;
     }
     (void)big;

@@ -222,6 +222,7 @@ def main():
     ap.add_argument("--cpu-images", type=int, default=4, help="images for the CPU baseline + parity (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="concurrent image chunks per GPU (HIP streams)")
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -242,8 +243,13 @@ def main():
     T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
     gathered = torch.empty(world * B, device=dev) if world > 1 else None
 
+    run = None if args.no_graph else eng.graphed_predict(B, S, "Industrial", streams=args.streams)
+
     def step():
-        maps, score = eng.predict(x, T, "Industrial", streams=args.streams)
+        if run is not None:
+            maps, score = run(x, T)
+        else:
+            maps, score = eng.predict(x, T, "Industrial", streams=args.streams)
         if world > 1:
             dist.all_gather_into_tensor(gathered, score)
         return maps
@@ -287,7 +293,7 @@ def main():
                                "Industrial blur, per-GPU batch of images",
                    "global_batch": B * world, "img_size": S, "per_gpu_batch": B,
                    "parallelism": f"image-sharded dp{world} (+RCCL all-gather of image scores)",
-                   "streams_per_gpu": args.streams,
+                   "streams_per_gpu": args.streams, "hipgraph": not args.no_graph,
                    "gflop_per_image": round(flops_per_image((S // 14) ** 2 + 1) / 1e9, 2)},
     }
     line["tflops_whole_path"] = round(flops_per_image((S // 14) ** 2 + 1) * images / elapsed / 1e12, 1)

@@ -16,6 +16,8 @@ every fixture here is "reference code on synthetic weights". Outputs:
                     (forward_utils.py:138-162, model/adapter.py:114-145)
   golden_ops.npz    per-op known-answer vectors (LayerNorm, residual blocks,
                     adapter blend, similarity map incl. train branch, metrics_eval)
+  golden_c5.npz     config-C5 shapes: 448 px (1025 tokens), 6 levels [4..24],
+                    relu=True projections, Medical-domain map, B=1
   ../../aa-clip_amd/model/prompt_tokens.json   token ids of every prompt the
                     reference can build (tokenizer.py:150-185 over
                     dataset/constants.py:78-148)
@@ -51,7 +53,7 @@ def t(a):
     return torch.from_numpy(np.ascontiguousarray(a))
 
 
-def build_reference(relu=False, levels=(6, 12, 18, 24)):
+def build_reference(relu=False, levels=(6, 12, 18, 24), img_size=336):
     prev = os.getcwd()
     os.chdir(REF)  # the reference resolves ./dataset/metadata relative to cwd
     try:
@@ -59,8 +61,10 @@ def build_reference(relu=False, levels=(6, 12, 18, 24)):
         from model.adapter import AdaptedCLIP
     finally:
         os.chdir(prev)
-    clip = create_model("ViT-L-14-336", 336, pretrained=None, device="cpu")
-    sd = synth.clip_state_dict(SEED)
+    # the random-init branch ignores img_size; force_image_size sets the grid (clip.py:159-161)
+    clip = create_model("ViT-L-14-336", img_size, pretrained=None, device="cpu",
+                        force_image_size=img_size if img_size != 336 else None)
+    sd = synth.clip_state_dict(SEED, img_size=img_size)
     clip.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
     clip.eval()
     model = AdaptedCLIP(clip, text_adapt_weight=0.1, image_adapt_weight=0.1, text_adapt_until=3,
@@ -233,7 +237,23 @@ def main():
     ops["met_masks"], ops["met_labels"], ops["met_pp"], ops["met_ip"] = mk, lab, pp, ip
     ops["met_result"] = np.array(json.dumps(res))
     np.savez_compressed(os.path.join(HERE, "golden_ops.npz"), meta=json.dumps(meta), **ops)
-    for fn in ("golden_e2e.npz", "golden_text.npz", "golden_ops.npz"):
+
+    # ---------------------------------------------------------------- C5 shapes: 448 px, 6 levels, relu proj
+    lv6 = (4, 8, 12, 16, 20, 24)
+    _, model448, sd448, ia448, _ = build_reference(relu=True, levels=lv6, img_size=448)
+    x448 = synth.images(SEED, 1, 448)
+    seg, det = model448(t(x448))
+    T = t(text["bottle_T_adapted"])
+    c5 = dict(
+        levels=np.array(lv6), image_sha=np.array(synth.state_checksum({"x": x448})),
+        clip_sha=np.array(synth.state_checksum(sd448)), adapter_sha=np.array(synth.state_checksum(ia448)),
+        grid_A=np.stack([(100.0 * (f @ T)).numpy() for f in seg], axis=1).astype(np.float32),
+        det=det.numpy(), score=((det @ T)[:, 1].numpy() + 1) / 2,
+        map_med_sub=torch.cat([fu.calculate_similarity_map(f, T, 448, test=True, domain="Medical") for f in seg],
+                              1).sum(1).numpy()[:, ::8, ::8],
+    )
+    np.savez_compressed(os.path.join(HERE, "golden_c5.npz"), meta=json.dumps(meta), **c5)
+    for fn in ("golden_e2e.npz", "golden_text.npz", "golden_ops.npz", "golden_c5.npz"):
         print(fn, os.path.getsize(os.path.join(HERE, fn)))
 
 

@@ -97,3 +97,50 @@ def test_text_anchor_parity(dev, golden, weights, dtype):
             T = eng.class_anchor(torch.from_numpy(tx[f"{cls}_tok_normal"]).to(dev),
                                  torch.from_numpy(tx[f"{cls}_tok_abnormal"]).to(dev)).cpu().numpy()
             np.testing.assert_allclose(T, tx[f"{cls}_T_{key}"], atol=t_tol, rtol=t_tol * 10)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c5_shapes_parity(dev, golden, dtype):
+    """448 px (1025 tokens), 6 levels, relu projections: map vs the reference's golden."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_c5.npz"))
+    lv = tuple(int(v) for v in g["levels"])
+    sd = synth.clip_state_dict(111, img_size=448)
+    ia, _ = synth.adapter_state_dicts(111, relu=True, n_levels=len(lv))
+    vp = {k: torch.from_numpy(v).to(dev) for k, v in sd.items() if k.startswith("visual.")}
+    eng = VisualEngine(vp, {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}, levels=lv, dtype=dtype)
+    T = torch.from_numpy(golden["text"]["bottle_T_adapted"]).to(dev)
+    x = torch.from_numpy(synth.images(111, 1, 448)).to(dev)
+    maps, score = eng.predict(x, T, "Medical")
+    ref = g["map_med_sub"]
+    got = maps.cpu().numpy()[:, ::8, ::8]
+    err = np.abs(got - ref)
+    print(dtype, "c5 map max abs err", err.max())
+    if dtype == torch.float32:
+        assert err.max() < 1e-4
+        seg, det = eng.forward(x)
+        grid = np.stack([(100.0 * (f @ T)).cpu().numpy() for f in seg], axis=1)
+        np.testing.assert_allclose(grid, g["grid_A"], atol=5e-3)
+    else:
+        assert (err <= 3e-3 + 1.5e-2 * np.abs(ref)).all()
+    np.testing.assert_allclose(score.cpu().numpy(), g["score"], atol=1e-3)
+
+
+def test_graphed_predict_matches_eager(dev, weights):
+    """hipGraph replay (incl. the two-stream fork/join) gives bit-identical results."""
+    eng = _visual(weights, torch.bfloat16)
+    g = torch.Generator(device=dev).manual_seed(3)
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
+    for B, streams in ((1, 1), (4, 2)):
+        x = torch.randn(B, 3, 336, 336, device=dev, generator=g)
+        m0, s0 = [t.clone() for t in eng.predict(x, T, "Industrial", streams=streams)]
+        run = eng.graphed_predict(B, 336, "Industrial", streams=streams)
+        for _ in range(2):
+            m1, s1 = run(x, T)
+            torch.cuda.synchronize()
+            assert torch.equal(m1, m0) and torch.equal(s1, s0)
+        x2 = torch.randn(B, 3, 336, 336, device=dev, generator=g)
+        m2, _ = run(x2, T)
+        m2 = m2.clone()
+        m3, _ = eng.predict(x2, T, "Industrial", streams=streams)
+        assert torch.equal(m2, m3)

@@ -31,12 +31,13 @@ def test_gemm_bf16_plain(dev, M, N, K):
     assert err < 1e-3 * ref.abs().max().item() + 1e-4, err
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
-@pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (2000, 256, 64)])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (2000, 256, 64),
+                                   (18464, 3072, 1024), (577 * 40, 1024, 512)])
 def test_gemm_bf16_variants(dev, variant, M, N, K):
     """Every bf16 kernel family (2-stage 256x256, 4-phase 256x256, 2-stage 256x128)."""
     from aaclip import _lib
-    if variant in (1, 4) and N % 256:
+    if variant in (1, 4, 5) and N % 256:
         pytest.skip("256x256 tile needs N % 256 == 0")
     torch.manual_seed(M * 7 + N)
     a = torch.randn(M, K, device=dev).bfloat16()
@@ -62,9 +63,19 @@ def test_gemm_bf16_asymmetric_identity(dev):
     torch.testing.assert_close(out, w.float().T, atol=0, rtol=0)
 
 
-def test_gemm_epilogues_bf16(dev):
+@pytest.mark.parametrize("variant", [0, 4, 5])
+def test_gemm_epilogues_bf16(dev, variant):
+    from aaclip import _lib
+    _lib.call("aaclip_set_gemm_variant", variant)
+    try:
+        _epilogues(dev)
+    finally:
+        _lib.call("aaclip_set_gemm_variant", 0)
+
+
+def _epilogues(dev):
     torch.manual_seed(0)
-    M, N, K = 700, 1024, 1024
+    M, N, K = 20 * 577, 1024, 1024  # several tiles per persistent workgroup, ragged last M-tile
     a = torch.randn(M, K, device=dev).bfloat16()
     w = (torch.randn(N, K, device=dev) * 0.03).bfloat16()
     bias = torch.randn(N, device=dev)
