@@ -23,8 +23,11 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);
 }
+// one v_cvt_pk_bf16_f32 (RNE) for the pair; the scalar form costs 2 cvt + shift + or
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2v_t));
 }
 
 // ---------------------------------------------------------------- wave reductions

@@ -50,21 +50,19 @@ __device__ __forceinline__ float gelu_erf(float v) {
   return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
 }
 
-// GELU for the bf16 path: 1 + erf(z) through erfc(|z|) from Abramowitz-Stegun
-// 7.1.26 (|error| <= 1.5e-7, far below bf16's 2^-9 output rounding): one rcp,
-// one exp and a degree-5 polynomial instead of OCML's branchy erff, which
-// dominated the c_fc epilogue. For z < 0 the erfc form keeps GELU's small
-// negative tail accurate (no 1 - (1 - e) cancellation).
+// GELU for the bf16-input kernel: v * sigmoid(v * P(v^2)), P quadratic, fitted
+// (minimax on [-12, 12]) to the erf form: |error| <= 2.6e-5 absolute, an order
+// below the bf16 rounding of the output for |y| >= 0.01. The clamp keeps the
+// quintic in its monotone range (|v| > 8: sigmoid is 0/1 to 1e-12). 7 VALU + one
+// v_exp + one v_rcp per element, vs 16 + 2 for an erfc-polynomial form; the c_fc
+// epilogue is VALU-bound (all waves of the chip run it at once, no MFMA to hide
+// behind). -log2(e) is folded into the coefficients so v_exp_f32 (2^x) applies
+// directly. The fp32 parity kernel keeps the exact erff form (gelu_erf).
 __device__ __forceinline__ float gelu_fast(float v) {
-  const float z = v * 0.70710678118654752440f;
-  const float az = fabsf(z);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.0f));
-  float p = fmaf(t, 1.061405429f, -1.453152027f);
-  p = fmaf(t, p, 1.421413741f);
-  p = fmaf(t, p, -0.284496736f);
-  p = fmaf(t, p, 0.254829592f);
-  const float erfc_az = t * p * __expf(-az * az);
-  return 0.5f * v * (z >= 0.f ? 2.0f - erfc_az : erfc_az);
+  const float vc = __builtin_amdgcn_fmed3f(v, -8.0f, 8.0f);
+  const float s = vc * vc;
+  const float w = vc * fmaf(s, fmaf(s, 0.0010142630f, -0.10677572f), -2.3011212f);
+  return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(w));
 }
 
 // Epilogue on one element C[m, n] (m < M checked by the caller).
@@ -81,28 +79,6 @@ __device__ __forceinline__ void epilogue_store1(const GemmArgs& a, int m, int n,
   if (a.epi & AACLIP_EPI_AUX_BF16) ((uint16_t*)a.aux)[(size_t)orow * a.ldaux + n] = f32_to_bf16(v);
 }
 
-// Epilogue on 4 consecutive columns C[m, n..n+3] (n % 4 == 0).
-__device__ __forceinline__ void epilogue_store4(const GemmArgs& a, int m, int n, float4_t v) {
-  const int orow = remap_row(a, m);
-  if (a.epi & AACLIP_EPI_BIAS) v += *(const float4_t*)(a.bias + n);
-  if (a.epi & AACLIP_EPI_GELU)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = gelu_fast(v[j]);
-  if (a.epi & AACLIP_EPI_LEAKY)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = v[j] >= 0.f ? v[j] : 0.01f * v[j];
-  if (a.epi & AACLIP_EPI_RESID) v += *(const float4_t*)(a.res + (size_t)orow * a.ldr + n);
-  if (a.out_dtype == AACLIP_F32) {
-    *(float4_t*)((float*)a.C + (size_t)orow * a.ldc + n) = v;
-  } else {
-    *(uint2*)((uint16_t*)a.C + (size_t)orow * a.ldc + n) =
-        uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-  }
-  if (a.epi & AACLIP_EPI_AUX_BF16)
-    *(uint2*)((uint16_t*)a.aux + (size_t)orow * a.ldaux + n) =
-        uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-}
-
 // Bijective XCD remap (blocks b, b+8, ... share an XCD) + grouped tile order.
 __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, int& tm, int& tn,
                                             int GROUP_M = 8) {
@@ -117,6 +93,97 @@ __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, i
   const int in_group = wgid % per_group;
   tm = first_m + in_group % gsize;
   tn = in_group / gsize;
+}
+
+// Epilogue of one wave's (16*RM) x 64 output tile, staged through a wave-private
+// LDS slot ep[16][EP_LD] one 16-row block at a time (accumulator layout: lane
+// holds C[16i + 4*fq + e][16j + fr]; re-read row-major so every lane owns CPL
+// consecutive columns and issues 16-B stores: 8 bf16 or 4 fp32).
+// Latency, not bandwidth, bounds this phase (all waves of the chip reach it
+// together), and vmcnt retires in issue order, so a load issued after a store
+// cannot be waited on without also waiting for that store. Hence: the bias is
+// loaded once per tile before any store, and the residual rows of block i+1 are
+// loaded before block i's stores are issued (one block of prefetch).
+constexpr int EP_LD = 64 + 4;  // floats per staged row (pad: conflict-free writes)
+
+// EPI >= 0: compile-time epilogue flags (AACLIP_EPI_* | EPI_REMAP) so each used
+// combination is straight-line code; EPI = -1: flags read at run time (any combination).
+constexpr int EPI_REMAP = 64;
+
+template <int RM, int RN, bool BF16OUT, int EPI>
+__device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)[RM][RN], float* ep,
+                                              int mw, int nw, int lane) {
+  static_assert(RN == 4, "wave tile is 64 columns wide");
+  constexpr int CPL = BF16OUT ? 8 : 4;  // consecutive columns per lane
+  constexpr int LPR = 64 / CPL;         // lanes per staged row
+  constexpr int RPP = 64 / LPR;         // rows per pass
+  constexpr int NP = 16 / RPP;          // passes per 16-row block
+  constexpr int NV = CPL / 4;           // float4 per lane per pass
+  const int fr = lane & 15, fq = lane >> 4;
+  const int col = (lane % LPR) * CPL, rsub = lane / LPR;
+  const int n = nw + col;
+  const int epi = EPI >= 0 ? EPI : a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
+  const bool full = mw + 16 * RM <= a.M;
+  auto out_row = [&](int m) { return (epi & EPI_REMAP) ? remap_row(a, m) : m; };
+  float4_t bias[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    bias[v] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)(a.bias + n + 4 * v) : float4_t{0.f, 0.f, 0.f, 0.f};
+  float4_t res[2][NP][NV];
+  auto load_res = [&](int i, float4_t (&dst)[NP][NV]) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int m = mw + i * 16 + p * RPP + rsub;
+      const float* src = a.res + (size_t)out_row(min(m, a.M - 1)) * a.ldr + n;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) dst[p][v] = *(const float4_t*)(src + 4 * v);
+    }
+  };
+  if (epi & AACLIP_EPI_RESID) load_res(0, res[0]);
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ep[(fq * 4 + e) * EP_LD + j * 16 + fr] = acc[i][j][e];
+    if ((epi & AACLIP_EPI_RESID) && i + 1 < RM) load_res(i + 1, res[(i + 1) & 1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int r = p * RPP + rsub;
+      const int m = mw + i * 16 + r;
+      float4_t v[NV];
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        v[q] = *(const float4_t*)(ep + r * EP_LD + col + 4 * q) + bias[q];
+        if (epi & AACLIP_EPI_GELU)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[q][t] = gelu_fast(v[q][t]);
+        if (epi & AACLIP_EPI_LEAKY)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[q][t] = v[q][t] >= 0.f ? v[q][t] : 0.01f * v[q][t];
+        if (epi & AACLIP_EPI_RESID) v[q] += res[i & 1][p][q];
+      }
+      if (full || m < a.M) {
+        const size_t orow = (size_t)out_row(m);
+        if constexpr (BF16OUT) {
+          *(uint4*)((uint16_t*)a.C + orow * a.ldc + n) =
+              uint4{pack_bf16x2(v[0][0], v[0][1]), pack_bf16x2(v[0][2], v[0][3]),
+                    pack_bf16x2(v[1][0], v[1][1]), pack_bf16x2(v[1][2], v[1][3])};
+        } else {
+#pragma unroll
+          for (int q = 0; q < NV; ++q) *(float4_t*)((float*)a.C + orow * a.ldc + n + 4 * q) = v[q];
+        }
+        if (epi & AACLIP_EPI_AUX_BF16) {
+#pragma unroll
+          for (int q = 0; q < NV; ++q)
+            *(uint2*)((uint16_t*)a.aux + orow * a.ldaux + n + 4 * q) =
+                uint2{pack_bf16x2(v[q][0], v[q][1]), pack_bf16x2(v[q][2], v[q][3])};
+        }
+      }
+    }
+  }
 }
 
 // ============================================================== bf16 MFMA kernel
@@ -224,376 +291,37 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue, staged through LDS one 16-row block at a time so that each lane
-  // finishes 4 consecutive columns (16-B fp32 / 8-B bf16 stores, coalesced rows).
-  // Accumulator layout: lane holds C[16i + 4*fq + e][16j + fr]. Each wave stages
-  // through its own LDS slot (the main loop's last barrier freed the tiles), so
-  // no workgroup barrier is needed: LDS ops of one wave execute in order, and the
-  // asm memory fences keep the compiler from reordering the write/read phases.
-  constexpr int EP_LD = TN + 4;  // floats per staged row (pad: conflict-free writes)
-  float* ep = (float*)smem + wid * 16 * EP_LD;
-  constexpr int F4_PER_ROW = TN / 4;
-  if (a.dbg & 1) {  // diagnostic timing build path: keep the MFMA results live, store nothing
+  if (a.dbg & 1) {  // diagnostic timing path: keep the MFMA results live, store nothing
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
       for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-#pragma unroll
-  for (int i = 0; i < RM; ++i) {
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ep[(fq * 4 + e) * EP_LD + j * 16 + fr] = acc[i][j][e];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (int f = lane; f < 16 * F4_PER_ROW; f += 64) {
-      const int r = f / F4_PER_ROW, c4 = f % F4_PER_ROW;
-      const int m = m0 + wm * TM + i * 16 + r;
-      if (m < a.M) {
-        const float4_t v = *(const float4_t*)(ep + r * EP_LD + c4 * 4);
-        epilogue_store4(a, m, n0 + wn * TN + c4 * 4, v);
-      }
-    }
-  }
-}
-
-// ============================================================== bf16 MFMA, persistent
-// Same tile / main loop as gemm_bf16_kernel, but each workgroup loops over the
-// tiles L = blockIdx.x, blockIdx.x + gridDim.x, ... (gridDim.x = #CUs; the
-// linear id keeps the XCD-aware order of tile_coords). Tile seams are
-// pipelined: during the last K-step of tile i the DMA of tile i+1's first
-// K-stage is issued into the free buffer; tile i's epilogue stages through the
-// buffer just consumed; tile i+1's first barrier waits with vmcnt(NSTORE), not 0.
-// vmcnt retires in issue order and the prefetch is older than the epilogue's
-// stores, so the wait guarantees the prefetch landed while up to NSTORE of the
-// previous tile's output stores keep draining behind the next main loop.
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_persistent_kernel(GemmArgs a) {
-  constexpr int NWAVES = WM * WN;
-  constexpr int BK = 64;
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int RM = TM / 16, RN = TN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int A_LOADS = A_BYTES / (NWAVES * 1024);
-  constexpr int B_LOADS = B_BYTES / (NWAVES * 1024);
-  constexpr int EP_LD = TN + 4, F4_PER_ROW = TN / 4;
-  constexpr int STORES_PER_WAVE = RM * (16 * F4_PER_ROW / 64);  // C stores per wave per tile
-  static_assert(A_LOADS * NWAVES * 1024 == A_BYTES && B_LOADS * NWAVES * 1024 == B_BYTES, "tile");
-  static_assert((16 * F4_PER_ROW) % 64 == 0, "epilogue store count must be lane-uniform");
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int ntiles = a.tiles_m * a.tiles_n;
-  const int nk = a.K / BK;
-  const uint16_t* __restrict__ Ag = (const uint16_t*)a.A;
-  const uint16_t* __restrict__ Wg = (const uint16_t*)a.W;
-
-  const uint16_t* a_src[A_LOADS];
-  const uint16_t* b_src[B_LOADS];
-  auto set_sources = [&](int m0_, int n0_) {
-#pragma unroll
-    for (int i = 0; i < A_LOADS; ++i) {
-      const int r = (i * NWAVES + wid) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (r & 7);
-      a_src[i] = Ag + (size_t)min(m0_ + r, a.M - 1) * a.lda + c * 8;
-    }
-#pragma unroll
-    for (int i = 0; i < B_LOADS; ++i) {
-      const int r = (i * NWAVES + wid) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (r & 7);
-      b_src[i] = Wg + (size_t)(n0_ + r) * a.ldw + c * 8;
-    }
-  };
-#define PGEMM_STAGE(kt, buf)                                                                   \
-  do {                                                                                         \
-    char* base_ = smem + (buf) * STAGE_BYTES;                                                  \
-    const int koff_ = (kt) * BK;                                                               \
-    _Pragma("unroll") for (int i = 0; i < A_LOADS; ++i)                                        \
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + koff_),                        \
-                                       LDS_PTR(base_ + (i * NWAVES + wid) * 1024), 16, 0, 0);   \
-    _Pragma("unroll") for (int i = 0; i < B_LOADS; ++i)                                        \
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + koff_),                        \
-                                       LDS_PTR(base_ + A_BYTES + (i * NWAVES + wid) * 1024),   \
-                                       16, 0, 0);                                              \
-  } while (0)
-
-  int a_off[RM][2], b_off[RN][2];
-#pragma unroll
-  for (int i = 0; i < RM; ++i) {
-    const int r = wm * TM + i * 16 + fr;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) a_off[i][kk] = r * 128 + (((kk * 4 + fq) ^ (r & 7)) << 4);
-  }
-#pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int r = wn * TN + j * 16 + fr;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) b_off[j][kk] = A_BYTES + r * 128 + (((kk * 4 + fq) ^ (r & 7)) << 4);
-  }
-
-  int L = blockIdx.x;
-  if (L >= ntiles) return;
-  int tm, tn;
-  tile_coords(L, a.tiles_m, a.tiles_n, tm, tn);
-  set_sources(tm * BM, tn * BN);
-  int it = 0;  // running K-step counter: buffer parity continues across tiles
-  PGEMM_STAGE(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  bool pending_stores = false;
-
-  while (true) {
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int Ln = L + gridDim.x;
-    const bool has_next = Ln < ntiles;
-    int tm_n = 0, tn_n = 0;
-    if (has_next) tile_coords(Ln, a.tiles_m, a.tiles_n, tm_n, tn_n);
-    if (pending_stores) {
-      // the previous tile's prefetch (older) must have landed; its stores may drain
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(STORES_PER_WAVE < 63 ? STORES_PER_WAVE : 63)
-                   : "memory");
-    }
-    float4_t acc[RM][RN];
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt, ++it) {
-      const int cur = it & 1;
-      if (kt + 1 < nk) {
-        PGEMM_STAGE(kt + 1, cur ^ 1);
-      } else if (has_next) {
-        set_sources(tm_n * BM, tn_n * BN);  // current tile's DMA all issued: retarget
-        PGEMM_STAGE(0, cur ^ 1);
-      }
-      const char* base = smem + cur * STAGE_BYTES;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t bf[RN];
-#pragma unroll
-        for (int j = 0; j < RN; ++j) bf[j] = *(const bf16x8_t*)(base + b_off[j][kk]);
-#pragma unroll
-        for (int i = 0; i < RM; ++i) {
-          const bf16x8_t af = *(const bf16x8_t*)(base + a_off[i][kk]);
-#pragma unroll
-          for (int j = 0; j < RN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
-        }
-      }
-      if (kt + 1 < nk)
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      else  // all reads of `cur` done before it becomes the epilogue staging area
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    // ---- epilogue through the just-consumed buffer (the other one is loading)
-    float* ep = (float*)(smem + ((it - 1) & 1) * STAGE_BYTES) + wid * 16 * EP_LD;
-    const bool full_tile = m0 + BM <= a.M;
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int j = 0; j < RN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) ep[(fq * 4 + e) * EP_LD + j * 16 + fr] = acc[i][j][e];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      for (int f = lane; f < 16 * F4_PER_ROW; f += 64) {
-        const int r = f / F4_PER_ROW, c4 = f % F4_PER_ROW;
-        const int m = m0 + wm * TM + i * 16 + r;
-        if (full_tile || m < a.M) {
-          const float4_t v = *(const float4_t*)(ep + r * EP_LD + c4 * 4);
-          epilogue_store4(a, m, n0 + wn * TN + c4 * 4, v);
-        }
-      }
-    }
-    if (!has_next) break;
-    // a partial tile issued fewer stores than the counted wait assumes: drain fully
-    if (!full_tile) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // epilogue LDS reads done before the barrier
-    pending_stores = true;
-    L = Ln;
-    tm = tm_n;
-    tn = tn_n;
-  }
-#undef PGEMM_STAGE
-}
-
-// ============================================================== bf16 MFMA, 4-phase pipeline
-// 256x256x64 tile, 8 waves (2 along M x 4 along N, wave tile 128x64 = 8x4
-// MFMA tiles). Each K-tile is computed in 4 phases, one 64x32 quadrant of the
-// wave tile (16 MFMAs) per phase:
-//   P1 (A lo, B lo)   P2 (A lo, B hi)   P3 (A hi, B hi)   P4 (A hi, B lo)
-// The LDS image of one K-tile is cut into 4 regions of 128 rows x 128 B by the
-// phase that first reads them, across waves:
-//   R1 = A lo rows of both M-halves, R2 = B lo rows of all 4 N-quarters,
-//   R3 = B hi rows, R4 = A hi rows.
-// Phase p of K-tile t issues region R_p of K-tile t+1 (2 LDS-DMA instructions
-// per wave) into the other buffer, then runs its MFMAs, then waits with a
-// COUNTED vmcnt(4) — two regions stay in flight across the barrier — before the
-// one raw s_barrier of the phase. Every region therefore has >= 3 phases between
-// issue and first read (P1->P1, P2->P1, P3->P2, P4->P3), and its buffer slot was
-// last read >= 1 barrier earlier (R1: P2, R2: P4, R3: P2, R4: P3 of tile t-1).
-// The last K-tile drains with vmcnt(0).
-__device__ __forceinline__ int reg_a_row(int q, int hi) {  // region row -> tile row (A)
-  return (q >> 6) * 128 + hi * 64 + (q & 63);
-}
-__device__ __forceinline__ int reg_b_row(int q, int hi) {  // region row -> tile row (B / n)
-  return (q >> 5) * 64 + hi * 32 + (q & 31);
-}
-
-#define VM_WAIT_BARRIER(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_barrier" ::: "memory")
-
-__global__ __launch_bounds__(512) void gemm_bf16_4ph_kernel(GemmArgs a) {
-  constexpr int REG = 128 * 128;      // bytes per region
-  constexpr int STAGE = 4 * REG;      // R1 R2 R3 R4
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
-  int tm, tn;
-  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const uint16_t* __restrict__ Ag = (const uint16_t*)a.A;
-  const uint16_t* __restrict__ Wg = (const uint16_t*)a.W;
-
-  // DMA sources: region rows q = (piece)*8 + lane/8 for pieces wid and wid+8;
-  // physical chunk lane%8 holds logical chunk (lane%8) ^ (q&7).
-  const uint16_t* src[4][2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int q = (wid + 8 * k) * 8 + (lane >> 3);
-    const int c = ((lane & 7) ^ (q & 7)) * 8;
-    src[0][k] = Ag + (size_t)min(m0 + reg_a_row(q, 0), a.M - 1) * a.lda + c;  // R1
-    src[1][k] = Wg + (size_t)(n0 + reg_b_row(q, 0)) * a.ldw + c;              // R2
-    src[2][k] = Wg + (size_t)(n0 + reg_b_row(q, 1)) * a.ldw + c;              // R3
-    src[3][k] = Ag + (size_t)min(m0 + reg_a_row(q, 1), a.M - 1) * a.lda + c;  // R4
-  }
-#define ISSUE_REGION(r, kt, buf)                                                             \
-  do {                                                                                       \
-    char* dst_ = smem + (buf) * STAGE + (r) * REG;                                           \
-    const int ko_ = (kt) * 64;                                                               \
-    __builtin_amdgcn_global_load_lds((const void*)(src[r][0] + ko_), LDS_PTR(dst_ + wid * 1024), 16, 0, 0); \
-    __builtin_amdgcn_global_load_lds((const void*)(src[r][1] + ko_), LDS_PTR(dst_ + (wid + 8) * 1024), 16, 0, 0); \
-  } while (0)
-
-  const int fr = lane & 15, fq = lane >> 4;
-  // fragment byte offsets inside a region (row q, logical chunk kk*4+fq)
-  auto roff = [&](int q, int kk) { return q * 128 + (((kk * 4 + fq) ^ (q & 7)) << 4); };
-  int aoff[4][2], boff[2][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) aoff[i][kk] = roff(wm * 64 + i * 16 + fr, kk);
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) boff[j][kk] = roff(wn * 32 + j * 16 + fr, kk);
-
-  float4_t acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = a.K / 64;
-  ISSUE_REGION(0, 0, 0);
-  ISSUE_REGION(1, 0, 0);
-  ISSUE_REGION(2, 0, 0);
-  ISSUE_REGION(3, 0, 0);
-  VM_WAIT_BARRIER(0);
-
-  bf16x8_t af[4][2], bf[2][2];
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* st = smem + (kt & 1) * STAGE;
-    const bool more = kt + 1 < nk;
-    const int nb = (kt + 1) & 1;
-    // ---- P1: A lo (R1) x B lo (R2)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = *(const bf16x8_t*)(st + REG + boff[j][kk]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = *(const bf16x8_t*)(st + aoff[i][kk]);
-    if (more) ISSUE_REGION(0, kt + 1, nb);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[i][j], 0, 0, 0);
-    if (more) VM_WAIT_BARRIER(4); else VM_WAIT_BARRIER(0);
-    // ---- P2: A lo (regs) x B hi (R3)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = *(const bf16x8_t*)(st + 2 * REG + boff[j][kk]);
-    if (more) ISSUE_REGION(1, kt + 1, nb);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[i][2 + j], 0, 0, 0);
-    if (more) VM_WAIT_BARRIER(4); else VM_WAIT_BARRIER(0);
-    // ---- P3: A hi (R4) x B hi (regs)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = *(const bf16x8_t*)(st + 3 * REG + aoff[i][kk]);
-    if (more) ISSUE_REGION(2, kt + 1, nb);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[4 + i][2 + j], 0, 0, 0);
-    if (more) VM_WAIT_BARRIER(6); else VM_WAIT_BARRIER(0);
-    // ---- P4: A hi (regs) x B lo (R2 re-read)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = *(const bf16x8_t*)(st + REG + boff[j][kk]);
-    if (more) ISSUE_REGION(3, kt + 1, nb);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[4 + i][j], 0, 0, 0);
-    if (more) VM_WAIT_BARRIER(4); else VM_WAIT_BARRIER(0);
-  }
-#undef ISSUE_REGION
-
-  // ---- epilogue (LDS free: every DMA retired by the final vmcnt(0) + barrier)
-  constexpr int TN = 64, EP_LD = TN + 4, F4_PER_ROW = TN / 4;
+  // The main loop's last barrier freed the LDS tiles: each wave stages through
+  // its own slot, no workgroup barrier needed.
   float* ep = (float*)smem + wid * 16 * EP_LD;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ep[(fq * 4 + e) * EP_LD + j * 16 + fr] = acc[i][j][e];
-    __syncthreads();
-    for (int f = lane; f < 16 * F4_PER_ROW; f += 64) {
-      const int r = f / F4_PER_ROW, c4 = f % F4_PER_ROW;
-      const int m = m0 + wm * 128 + i * 16 + r;
-      if (m < a.M) {
-        const float4_t v = *(const float4_t*)(ep + r * EP_LD + c4 * 4);
-        epilogue_store4(a, m, n0 + wn * TN + c4 * 4, v);
-      }
-    }
+  const int mw = m0 + wm * TM, nw = n0 + wn * TN;
+  const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
+#define EPI_CASE(BF, E)                                                \
+  if (bf16_out == (BF) && key == (E)) {                                \
+    wave_epilogue<RM, RN, BF, E>(a, acc, ep, mw, nw, lane);            \
+    return;                                                            \
   }
+  // the combinations the visual/text engines issue (engine.py)
+  const bool bf16_out = a.out_dtype != AACLIP_F32;
+  EPI_CASE(true, AACLIP_EPI_BIAS)                                        // qkv
+  EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)                      // c_fc
+  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)                    // out-proj, c_proj
+  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)  // c_proj + bf16 copy
+  EPI_CASE(false, AACLIP_EPI_LEAKY)                                      // adapters, seg/det proj
+  EPI_CASE(false, 0)                                                     // seg/det proj (no relu)
+  EPI_CASE(false, EPI_REMAP)                                             // patch embedding
+#undef EPI_CASE
+  if (bf16_out)
+    wave_epilogue<RM, RN, true, -1>(a, acc, ep, mw, nw, lane);
+  else
+    wave_epilogue<RM, RN, false, -1>(a, acc, ep, mw, nw, lane);
 }
 
 // ============================================================== fp32 MFMA kernel
@@ -671,53 +399,6 @@ int launch_bf16(GemmArgs a, hipStream_t s) {
   return AACLIP_OK;
 }
 
-int launch_bf16_4ph(GemmArgs a, hipStream_t s) {
-  if (a.N % 256) return AACLIP_ERR_ARG;
-  a.tiles_m = ceil_div(a.M, 256);
-  a.tiles_n = a.N / 256;
-  const size_t lds = 2 * 4 * 128 * 128;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_4ph_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
-      return AACLIP_ERR_LAUNCH;
-    attr_set = true;
-  }
-  gemm_bf16_4ph_kernel<<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
-  AACLIP_CHECK_LAUNCH();
-  return AACLIP_OK;
-}
-
-int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
-template <int BM, int BN, int WM, int WN>
-int launch_bf16_persistent(GemmArgs a, hipStream_t s) {
-  if (a.N % BN) return AACLIP_ERR_ARG;
-  a.tiles_m = ceil_div(a.M, BM);
-  a.tiles_n = a.N / BN;
-  const int ntiles = a.tiles_m * a.tiles_n;
-  const size_t lds = 2 * (size_t)(BM + BN) * 64 * 2;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_persistent_kernel<BM, BN, WM, WN>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return AACLIP_ERR_LAUNCH;
-    attr_set = true;
-  }
-  const int grid = min(ntiles, num_cus());
-  gemm_bf16_persistent_kernel<BM, BN, WM, WN><<<grid, WM * WN * 64, lds, s>>>(a);
-  AACLIP_CHECK_LAUNCH();
-  return AACLIP_OK;
-}
 
 int g_gemm_variant = 0;  // tuning hook (aaclip_set_gemm_variant); 0 = default dispatch
 int g_group_m = 8;
@@ -727,9 +408,10 @@ int g_dbg = 0;
 }  // namespace
 
 extern "C" int aaclip_set_gemm_variant(int variant) {
-  // bits 0-3: kernel family; bits 4-7: tile-order group height (0 = 8); bit 8: setprio
+  // bits 0-3: tile family (0 default, 1 = 256x256, 2 = 256x128); bits 4-7: tile-order
+  // group height (0 = 8); bit 8: setprio around the MFMA cluster; bit 9: skip epilogue
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || fam > 5) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 1024 || fam > 2) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 8;
   g_setprio = (variant >> 8) & 1;
@@ -758,18 +440,11 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
   hipStream_t s = (hipStream_t)stream;
   if (in_dtype == AACLIP_BF16) {
     AACLIP_REQUIRE(K % 64 == 0 && N % 128 == 0);
-    // 256x256 tiles when they fill the chip; 256x128 otherwise (N = 768/1024 GEMMs)
-    const long t256 = (long)ceil_div(M, 256) * (N / 256);
-    const bool big = N % 256 == 0 && t256 >= 2 * 256;
     switch (g_gemm_variant) {
-      case 1: return launch_bf16<256, 256, 2, 4>(a, s);                                  // 2-stage only
-      case 2: return N % 256 == 0 ? launch_bf16_4ph(a, s) : launch_bf16<256, 128, 4, 2>(a, s);  // 4-phase always
-      case 3: return launch_bf16<256, 128, 4, 2>(a, s);
-      case 4: return N % 256 == 0 ? launch_bf16<320, 256, 2, 4>(a, s) : launch_bf16<256, 128, 4, 2>(a, s);
-      case 5: return N % 256 == 0 ? launch_bf16_persistent<320, 256, 2, 4>(a, s) : launch_bf16<256, 128, 4, 2>(a, s);
+      case 1: return launch_bf16<256, 256, 2, 4>(a, s);
+      case 2: return launch_bf16<256, 128, 4, 2>(a, s);
       default: break;
     }
-    (void)big;
     // M = B*577 tiles badly by 256 (18464 = 72.1 x 256 at B=32: 3.42 waves of 256x256
     // tiles for N=3072, 1.14 for N=1024); 320-row tiles give 58 M-tiles -> 0.91 / 2.72 /
     // 3.63 waves for N = 1024 / 3072 / 4096 (measured 1.1-1.4x faster on every block GEMM).

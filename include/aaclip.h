@@ -66,9 +66,9 @@ int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K,
                 int row_group, int row_group_out, int row_offset, void* stream);
 
 /*
- * Tuning hook: select the bf16 GEMM kernel family for benchmarking. Bits 0-3:
- * 0 = default dispatch, 1 = 2-stage 256x256, 2 = 4-phase 256x256 (N % 256 == 0),
- * 3 = 2-stage 256x128, 4 = 2-stage 320x256, 5 = persistent 320x256; bits 4-7:
+ * Tuning hook: select the bf16 GEMM tile family for benchmarking. Bits 0-3:
+ * 0 = default dispatch (320x256 when N % 256 == 0, else 256x128),
+ * 1 = 256x256 (N % 256 == 0), 2 = 256x128; bits 4-7:
  * tile-order group height (0 = 8); bit 8: s_setprio around the MFMA cluster;
  * bit 9: diagnostic timing mode that skips the epilogue (outputs NOT written).
  * Process-global; not for production use.

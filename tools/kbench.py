@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--shapes", default="qkv,out,fc,proj,adapter", help="GEMM shapes to run")
     ap.add_argument("--map", action="store_true", help="also run the anomaly-map stream kernel (C2 sizes)")
+    ap.add_argument("--torch", action="store_true",
+                    help="also time torch (hipBLASLt) on the same GEMM shapes, for comparison only")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, n, W = args.batch, 577, 1024
@@ -73,6 +75,23 @@ def main():
                     if prev is None or ms < prev[0]:
                         res[key] = (ms, 2.0 * R * N * K / ms / 1e9)
         _lib.call("aaclip_set_gemm_variant", 0)
+        if args.torch:  # library comparison: linear (+bias) -> epilogue in torch ops
+            F = torch.nn.functional
+            for name, (N, K, kw, a, w, bias, out) in data.items():
+                bb = bias.bfloat16() if kw.get("bias") else None
+                x32 = torch.randn(R, N, device=dev) if kw.get("resid") else None
+                f0 = lambda: F.linear(a, w, bb)  # noqa: E731
+                if kw.get("gelu"):
+                    f = lambda: F.gelu(F.linear(a, w, bb))  # noqa: E731
+                elif kw.get("resid"):
+                    f = lambda: x32.add_(F.linear(a, w, bb))  # noqa: E731
+                elif kw.get("leaky"):
+                    f = lambda: F.leaky_relu(F.linear(a, w))  # noqa: E731
+                else:
+                    f = f0
+                for key, fn in ((f"{name}/torch-gemm", f0), (f"{name}/torch-full", f)):
+                    ms = timeit(fn, args.reps)
+                    res[key] = (ms, 2.0 * R * N * K / ms / 1e9)
     if args.only in ("", "attn"):
         qkv = rnd(R, 3 * W).bfloat16()
         o = torch.empty(R, W, device=dev, dtype=torch.bfloat16)
