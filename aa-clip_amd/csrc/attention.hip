@@ -42,12 +42,6 @@ __device__ __forceinline__ float max_over_groups(float v) {
   auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
-__device__ __forceinline__ float sum_over_groups(float v) {
-  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
 
 // One 64-key tile for one wave: NKB live 16-key blocks (1, 2 or 4), NQB live
 // 16-query blocks (1 or 2), MASK = tile needs the key-tail / causal mask.
@@ -56,9 +50,14 @@ __device__ __forceinline__ float sum_over_groups(float v) {
 // Scores stay unscaled until the exponent: max on raw S (the scale is > 0),
 // p = exp2(S * log2e/8 - m2) as one FMA + one v_exp_f32. The O rescale is
 // skipped when no row max in the wave moved (alpha == 1 everywhere).
+// The softmax denominator is one more MFMA per 32 keys: an all-ones A operand
+// against the same bf16 P^T fragment gives sum_k p[k][q] in every accumulator
+// row (lane-local, already reduced over keys), replacing 16 v_add per 16 queries
+// per tile on an issue-bound loop; numerator and denominator then use the same
+// bf16-rounded p.
 template <int NKB, int NQB, bool MASK>
 __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&qf)[2][2], float4_t (&ot)[2][4],
-                                          float (&m_run)[2], float (&l_run)[2], int key0, int q0, int N,
+                                          float (&m_run)[2], float4_t (&l_acc)[2], int key0, int q0, int N,
                                           int causal, int g, int c) {
   constexpr float sl2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
   const char* vt_lds = kt_lds + KT * 128;
@@ -104,24 +103,20 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
     const float m_old = m_run[qb];
     const float m_new = fmaxf(m_old, mx * sl2);
     m_run[qb] = m_new;
-    float ls = 0.f;
     float p[2 * NKS][4];
 #pragma unroll
     for (int kb = 0; kb < 2 * NKS; ++kb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i)
         p[kb][i] = kb < NKB ? __builtin_amdgcn_exp2f(fmaf(st[qb][kb < NKB ? kb : 0][i], sl2, -m_new)) : 0.f;
-        ls += p[kb][i];
-      }
     if (__builtin_amdgcn_ballot_w64(m_new != m_old) != 0) {  // wave-uniform
       const float alpha = __builtin_amdgcn_exp2f(m_old - m_new);
-      l_run[qb] *= alpha;
+      l_acc[qb][0] *= alpha;  // only element 0 is read at the end
 #pragma unroll
       for (int db = 0; db < 4; ++db)
 #pragma unroll
         for (int e = 0; e < 4; ++e) ot[qb][db][e] *= alpha;
     }
-    l_run[qb] += ls;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       bf16x8_t v;
@@ -133,6 +128,14 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
       pf[qb][ks] = v;
     }
   }
+  // l += 1 . P^T
+  const bf16x8_t ones = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                         (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb)
+      l_acc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qb][ks], l_acc[qb], 0, 0, 0);
   // O^T += V^T . P^T ; V^T fragment via transposing LDS reads
 #pragma unroll
   for (int db = 0; db < 4; ++db) {
@@ -152,10 +155,18 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
   }
 }
 
-__global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
+#ifndef ATTN_STAGES
+#define ATTN_STAGES 3  // K/V ring depth (LDS: ATTN_STAGES x 16 KiB per workgroup)
+#endif
+#ifndef ATTN_OCC
+#define ATTN_OCC 3  // workgroups per CU the register budget is sized for
+#endif
+
+__global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
                                                         uint16_t* __restrict__ out, int N, int H,
                                                         int causal) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * KT * 128];  // [stage][K|V][64][128B]
+  constexpr int NS = ATTN_STAGES;
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * KT * 128];  // [stage][K|V][64][128B]
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, c = lane & 15;
@@ -215,7 +226,7 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const uint16_t* __res
 #pragma unroll
     for (int db = 0; db < 4; ++db) ot[qb][db] = float4_t{0.f, 0.f, 0.f, 0.f};
   float m_run[2] = {-INFINITY, -INFINITY};
-  float l_run[2] = {0.f, 0.f};  // per-lane partial row sums (reduced over g at the end)
+  float4_t l_acc[2] = {float4_t{0.f, 0.f, 0.f, 0.f}, float4_t{0.f, 0.f, 0.f, 0.f}};  // row sums (MFMA)
 
   int ntiles = (N + KT - 1) / KT;
   if (causal) {
@@ -223,41 +234,55 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const uint16_t* __res
     ntiles = min(ntiles, last_q / KT + 1);
   }
 
+  // Ring of NS K/V stages: tile t+NS-1 is issued while tile t is computed; the
+  // end-of-tile wait is COUNTED (vmcnt retires in order, 4 DMAs per wave per
+  // stage) so tiles t+2.. stay in flight across the barrier.
+#define ATTN_WAIT_BARRIER(n) asm volatile("s_waitcnt vmcnt(" #n ")\n\ts_barrier" ::: "memory")
   stage(0, 0);
-  __syncthreads();
-  // wave-uniform work shape: query blocks with any valid row, key blocks of the tile
-  const int nqb = q0 + 16 < N ? 2 : (q0 < N ? 1 : 0);
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < ntiles) stage(t + 1, cur ^ 1);
+  if (NS > 2 && ntiles > 1) stage(1, 1);
+  if (NS > 2 && ntiles > 1) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
+  // Waves always compute both 16-query blocks (rows past N are clamped copies,
+  // discarded at the store); a wave with no valid query skips the math but keeps
+  // staging and barriers. Full tiles (no key tail, no causal cut for any wave of
+  // the workgroup) run one tile instance in a loop of their own: a per-tile
+  // dispatch over several instances costs ~40 accumulator register copies per tile
+  // on this issue-bound loop. The masked tail (key tail; causal diagonal) follows.
+  const bool active = q0 < N;
+  const int nfull = causal ? min(N / KT, (qtile * QT + 1) / KT) : N / KT;
+  int t = 0, cur = 0;
+  auto advance = [&]() {  // issue tile t+NS-1, then wait for tile t+1 and sync
+    const int nxt = t + NS - 1;
+    int nb = cur + NS - 1;
+    if (nb >= NS) nb -= NS;
+    if (nxt < ntiles) stage(nxt, nb);
+    return nxt < ntiles && NS > 2;
+  };
+  for (; t < nfull; ++t) {
+    const bool deep = advance();
+    if (active)
+      attn_tile<4, 2, false>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g, c);
+    if (deep) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
+    cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+  for (; t < ntiles; ++t) {
+    const bool deep = advance();
     const char* kt_lds = smem + cur * (2 * KT * 128);
     const int key0 = t * KT;
-    const int live = min(KT, N - key0);               // valid keys in this tile
-    const bool masked = (live < KT) || (causal && key0 + KT - 1 > q0);
-    const int nkb = live > 32 ? 4 : (live > 16 ? 2 : 1);  // 16-key blocks to compute
-#define ATTN_TILE(NKB_, NQB_, M_) \
-    attn_tile<NKB_, NQB_, M_>(kt_lds, qf, ot, m_run, l_run, key0, q0, N, causal, g, c)
-    if (!masked) {
-      if (nqb == 2) ATTN_TILE(4, 2, false);
-      else if (nqb == 1) ATTN_TILE(4, 1, false);
-    } else if (nqb == 2) {
-      if (nkb == 4) ATTN_TILE(4, 2, true);
-      else if (nkb == 2) ATTN_TILE(2, 2, true);
-      else ATTN_TILE(1, 2, true);
-    } else if (nqb == 1) {
-      if (nkb == 4) ATTN_TILE(4, 1, true);
-      else if (nkb == 2) ATTN_TILE(2, 1, true);
-      else ATTN_TILE(1, 1, true);
+    const int live = min(KT, N - key0);  // valid keys in this tile
+    if (active) {
+      if (live > 32) attn_tile<4, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c);
+      else if (live > 16) attn_tile<2, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c);
+      else attn_tile<1, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c);
     }
-#undef ATTN_TILE
-    __syncthreads();
+    if (deep) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
+    cur = cur + 1 == NS ? 0 : cur + 1;
   }
+#undef ATTN_WAIT_BARRIER
 
   // ---- epilogue: O[q][d = db*16 + 4g + i] = ot / l
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    const float l = sum_over_groups(l_run[qb]);
-    const float inv = 1.0f / l;
+    const float inv = 1.0f / l_acc[qb][0];
     const int q = q0 + qb * 16 + c;
     if (q < N) {
       uint16_t* o = out + ((size_t)b * N + q) * HDt + h * HD_;
