@@ -254,3 +254,30 @@ def image_score(det_raw, batch, n_patch, partial, det=None, T=None, score=None, 
         raise ValueError("image_score shape mismatch")
     call("aaclip_image_score", dtag(det_raw), _ptr(det_raw), det_raw.stride(0), _ptr(T), batch, n_patch, C,
          int(normalize), _ptr(partial), _ptr(det), _ptr(score), _stream())
+
+
+def metrics_eval(pixel_preds: torch.Tensor, pixel_label: torch.Tensor, image_preds: torch.Tensor,
+                 image_label: torch.Tensor, *, medical: bool) -> list[float]:
+    """Device metrics_eval of one class (aaclip_metrics_eval): returns the unrounded
+    [pixel AUROC, pixel AP, image AUROC, image AP]. pixel_preds [N, ...] fp32 maps,
+    pixel_label same element count (nonzero = anomalous), image_* [N]."""
+    N = pixel_preds.shape[0]
+    preds = pixel_preds.reshape(N, -1).to(torch.float32).contiguous()
+    pix = preds.shape[1]
+    lab = pixel_label.reshape(N, -1)
+    if lab.shape[1] != pix:
+        raise ValueError("pixel_label and pixel_preds must have the same number of elements per image")
+    lab = (lab != 0).to(torch.uint8).contiguous()
+    ip = image_preds.reshape(-1).to(torch.float32).contiguous()
+    il = (image_label.reshape(-1) != 0).to(torch.uint8).contiguous()
+    if ip.numel() != N or il.numel() != N:
+        raise ValueError("image_preds / image_label must have one entry per image")
+    _dev(preds, lab, ip, il)
+    need = ctypes.c_size_t(0)
+    call("aaclip_metrics_workspace", N * pix, N, ctypes.byref(need))
+    ws = torch.empty(int(need.value) + 256, device=preds.device, dtype=torch.uint8)
+    off = (-ws.data_ptr()) % 256
+    out = torch.empty(4, device=preds.device, dtype=torch.float64)
+    call("aaclip_metrics_eval", _ptr(preds), _ptr(lab), _ptr(ip), _ptr(il), N, pix, int(medical),
+         ws.data_ptr() + off, need.value, _ptr(out), _stream())
+    return out.tolist()

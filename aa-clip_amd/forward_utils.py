@@ -9,8 +9,10 @@
       train: bilinear -> softmax over the two anchors).
   anomaly_map_multilevel     the fused form of test.py:86-93 (all levels in one
       stream kernel, level sum before blur+upsample).
-  metrics_eval               forward_utils.py:233-280, host-side (numpy/sklearn,
-      as in the reference; the §8(f)-1 "next" row moves it on device).
+  metrics_eval               forward_utils.py:233-280 — on device (aaclip_metrics_eval:
+      min-max normalisation, score fusion, radix-sorted exact tie-aware AUROC / AP,
+      identical to sklearn after the reference's 4-decimal rounding). numpy inputs
+      on a host without a GPU use the reference's own numpy/sklearn formulation.
 Training losses and visualize() (cv2) are out of scope.
 """
 from __future__ import annotations
@@ -100,31 +102,43 @@ def anomaly_map_multilevel(patch_features, epoch_text_feature, img_size, domain=
     return ops.anomaly_map(lv, T, out, grid, g=g, ksize=k, sigma=s, normalize=normalize)
 
 
-def metrics_eval(pixel_label: np.ndarray, image_label: np.ndarray, pixel_preds: np.ndarray,
-                 image_preds: np.ndarray, class_names: str, domain: str):
+def metrics_eval(pixel_label, image_label, pixel_preds, image_preds, class_names: str, domain: str):
+    """forward_utils.py:233-280. Tensors (or numpy arrays, when a GPU is present)
+    go through the device kernel; the rounding / dict layout are the reference's."""
+    tensors = any(isinstance(t, torch.Tensor) for t in (pixel_label, image_label, pixel_preds, image_preds))
+    if tensors or torch.cuda.is_available():
+        dev = next((t.device for t in (pixel_preds, pixel_label) if isinstance(t, torch.Tensor) and t.is_cuda),
+                   torch.device("cuda", torch.cuda.current_device()))
+        t = [x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x))
+             for x in (pixel_preds, pixel_label, image_preds, image_label)]
+        t = [x.to(dev, non_blocking=True) for x in t]
+        pauc, pap, iauc, iap = ops.metrics_eval(t[0], t[1], t[2], t[3], medical=(domain == "Medical"))
+        if pauc != pauc:  # NaN: one pixel class only, sklearn raises here
+            raise ValueError("Only one class present in y_true. ROC AUC score is not defined in that case.")
+    else:
+        pauc, pap, iauc, iap = _metrics_host(pixel_label, image_label, pixel_preds, image_preds, domain)
+    return {"class name": class_names, "pixel AUC": round(pauc, 4) * 100, "pixel AP": round(pap, 4) * 100,
+            "image AUC": round(iauc, 4) * 100, "image AP": round(iap, 4) * 100}
+
+
+def _metrics_host(pixel_label, image_label, pixel_preds, image_preds, domain):
+    """numpy/sklearn formulation of the reference (forward_utils.py:241-271), for
+    numpy inputs on a host without a GPU."""
     from sklearn.metrics import average_precision_score, roc_auc_score
     if pixel_preds.max() != 1:
         pixel_preds = (pixel_preds - pixel_preds.min()) / (pixel_preds.max() - pixel_preds.min())
     if image_preds.max() != 1:
         image_preds = (image_preds - image_preds.min()) / (image_preds.max() - image_preds.min())
-    pmax_pred = pixel_preds.max(axis=(1, 2))
-    if domain != "Medical":
-        image_preds = pmax_pred * 0.5 + image_preds * 0.5
-    else:
-        image_preds = pmax_pred
-    pixel_label = pixel_label.flatten()
-    pixel_preds = pixel_preds.flatten()
-    zero_pixel_auc = roc_auc_score(pixel_label, pixel_preds)
-    zero_pixel_ap = average_precision_score(pixel_label, pixel_preds)
+    pmax = pixel_preds.max(axis=(1, 2))
+    image_preds = pmax if domain == "Medical" else pmax * 0.5 + image_preds * 0.5
+    y, s = pixel_label.flatten(), pixel_preds.flatten()
+    pauc, pap = roc_auc_score(y, s), average_precision_score(y, s)
     if image_label.max() != image_label.min():
-        agg_image_auc = roc_auc_score(image_label.flatten(), image_preds.flatten())
-        agg_image_ap = average_precision_score(image_label.flatten(), image_preds.flatten())
+        iauc = roc_auc_score(image_label.flatten(), image_preds.flatten())
+        iap = average_precision_score(image_label.flatten(), image_preds.flatten())
     else:
-        agg_image_auc = 0
-        agg_image_ap = 0
-    return {"class name": class_names, "pixel AUC": round(zero_pixel_auc, 4) * 100,
-            "pixel AP": round(zero_pixel_ap, 4) * 100, "image AUC": round(agg_image_auc, 4) * 100,
-            "image AP": round(agg_image_ap, 4) * 100}
+        iauc = iap = 0
+    return pauc, pap, iauc, iap
 
 
 def visualize(pixel_label, pixel_preds, file_names, save_dir, dataset_name, class_name):

@@ -6,8 +6,8 @@ same flow, same outputs), running AdaptedCLIP on the MI355X kernels.
 
 Differences from the reference, all on the host side:
   * the per-batch loop calls the fused AdaptedCLIP.predict (map + score in one
-    device pass) and keeps results on the device until the class is done
-    (the reference syncs twice per batch, test.py:85,93);
+    device pass) and keeps results on the device (the reference syncs twice per
+    batch, test.py:85,93); metrics_eval ranks the class's pixels on the device;
   * checkpoints load with torch.load(weights_only=True);
   * --allow_random_init / --dataset synthetic run without the OpenAI weights.
 """
@@ -43,9 +43,9 @@ def get_predictions(model, class_text_embeddings, test_loader, device, img_size,
         pmap, score = model.predict(image, class_text_embeddings, DOMAINS[dataset])
         preds.append(pmap.clone())
         preds_image.append(score.clone())
-    preds = torch.cat(preds).cpu().numpy()
-    preds_image = torch.cat(preds_image).cpu().numpy()
-    return (np.concatenate(masks, axis=0), np.concatenate(labels, axis=0), preds, preds_image, file_names)
+    # maps and scores stay on the device: metrics_eval ranks them there
+    return (np.concatenate(masks, axis=0), np.concatenate(labels, axis=0), torch.cat(preds), torch.cat(preds_image),
+            file_names)
 
 
 def main(argv=None):
@@ -128,7 +128,7 @@ def main(argv=None):
                     model=model, class_text_embeddings=text_embeddings[class_name], test_loader=loader,
                     device=device, img_size=args.img_size, dataset=args.dataset)
             if args.visualize:
-                visualize(masks, preds, file_names, args.save_path, args.dataset, class_name=class_name)
+                visualize(masks, preds.cpu().numpy(), file_names, args.save_path, args.dataset, class_name=class_name)
             result = metrics_eval(masks, labels, preds, preds_image, class_name, domain=DOMAINS[args.dataset])
             df.loc[len(df)] = Series(result)
         df.loc[len(df)] = df.drop(columns=["class name"]).mean()

@@ -20,6 +20,7 @@
 #ifndef AACLIP_H_
 #define AACLIP_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -195,6 +196,25 @@ int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n_levels, in
 int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld, const float* T,
                        int batch, int n_patch, int channels, int normalize, float* partial,
                        float* det, float* score, void* stream);
+
+/*
+ * Device metrics_eval for one class (replaces forward_utils.py:233-280 + the
+ * sklearn roc_auc_score / average_precision_score it calls): class-global
+ * min-max normalisation of the maps (skipped when max == 1) and of the image
+ * scores, image score fusion (0.5 * pixel max + 0.5 * score, or pixel max when
+ * medical != 0), then exact tie-aware AUROC and AP for pixels and images.
+ * pixel_preds [n_images, pix_per_image] fp32, pixel_label [same] uint8 (nonzero =
+ * anomalous), image_preds [n_images] fp32, image_label [n_images] uint8.
+ * out: device double[4] = pixel AUROC, pixel AP, image AUROC, image AP (unrounded;
+ * the image pair is 0, 0 when all image labels are equal, as in the reference;
+ * the pixel pair is NaN when all pixel labels are equal, where sklearn raises).
+ * workspace: caller-owned device memory, 256-B aligned, of the size
+ * aaclip_metrics_workspace reports (about 24 bytes per pixel). Deterministic.
+ */
+int aaclip_metrics_workspace(int64_t n_pixels, int n_images, size_t* bytes);
+int aaclip_metrics_eval(const float* pixel_preds, const uint8_t* pixel_label, const float* image_preds,
+                        const uint8_t* image_label, int n_images, int64_t pix_per_image, int medical,
+                        void* workspace, size_t workspace_bytes, double* out, void* stream);
 
 #ifdef __cplusplus
 }
