@@ -95,92 +95,88 @@ __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, i
   tn = in_group / gsize;
 }
 
-// Epilogue of one wave's (16*RM) x 64 output tile, staged through a wave-private
-// LDS slot ep[16][EP_LD] one 16-row block at a time (accumulator layout: lane
-// holds C[16i + 4*fq + e][16j + fr]; re-read row-major so every lane owns CPL
-// consecutive columns and issues 16-B stores: 8 bf16 or 4 fp32).
-// Latency, not bandwidth, bounds this phase (all waves of the chip reach it
-// together), and vmcnt retires in issue order, so a load issued after a store
-// cannot be waited on without also waiting for that store. Hence: the bias is
-// loaded once per tile before any store, and the residual rows of block i+1 are
-// loaded before block i's stores are issued (one block of prefetch).
-constexpr int EP_LD = 64 + 4;  // floats per staged row (pad: conflict-free writes)
+// Epilogue of one wave's (16*RM) x 64 output tile straight from the accumulators.
+// The main loop issues the MFMA with the W fragment as the first operand, so it
+// computes the tile transposed: lane (fr, fq) holds C[16i + fr][16j + 4fq + e],
+// e = 0..3 -- one row, 4 consecutive columns. fp32 rows leave as one 16-B store per
+// (i, j); bf16 rows are packed to 8 B and paired across column tiles j, j+1 with
+// v_permlane16_swap (lanes fq even/odd exchange halves) into 16-B stores. No LDS
+// round trip and no lgkmcnt waits: the measured LDS-staged form spent more time
+// staging than storing. The residual rows of tile-row i+1 are loaded before tile-row
+// i's stores (vmcnt retires in issue order).
+constexpr int EPI_REMAP = 64;
+
+__device__ __forceinline__ uint4 pair_bf16(const float4_t& lo, const float4_t& hi, int fq) {
+  // lo = this lane's 4 columns of tile j0, hi = of tile j1 (both row fr, cols 4fq..4fq+3)
+  uint32_t a0 = pack_bf16x2(lo[0], lo[1]), a1 = pack_bf16x2(lo[2], lo[3]);
+  uint32_t b0 = pack_bf16x2(hi[0], hi[1]), b1 = pack_bf16x2(hi[2], hi[3]);
+  auto x = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+  auto y = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+  // fq even: tile j0 cols 8(fq/2)..+7; fq odd: tile j1 cols 8(fq/2)..+7
+  (void)fq;
+  return uint4{x[0], y[0], x[1], y[1]};
+}
 
 // EPI >= 0: compile-time epilogue flags (AACLIP_EPI_* | EPI_REMAP) so each used
 // combination is straight-line code; EPI = -1: flags read at run time (any combination).
-constexpr int EPI_REMAP = 64;
-
 template <int RM, int RN, bool BF16OUT, int EPI>
-__device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)[RM][RN], float* ep,
-                                              int mw, int nw, int lane) {
-  static_assert(RN == 4, "wave tile is 64 columns wide");
-  constexpr int CPL = BF16OUT ? 8 : 4;  // consecutive columns per lane
-  constexpr int LPR = 64 / CPL;         // lanes per staged row
-  constexpr int RPP = 64 / LPR;         // rows per pass
-  constexpr int NP = 16 / RPP;          // passes per 16-row block
-  constexpr int NV = CPL / 4;           // float4 per lane per pass
+__device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
+                                              int lane) {
+  static_assert(RN % 2 == 0, "column tiles are paired");
   const int fr = lane & 15, fq = lane >> 4;
-  const int col = (lane % LPR) * CPL, rsub = lane / LPR;
-  const int n = nw + col;
   const int epi = EPI >= 0 ? EPI : a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
-  const bool full = mw + 16 * RM <= a.M;
   auto out_row = [&](int m) { return (epi & EPI_REMAP) ? remap_row(a, m) : m; };
-  float4_t bias[NV];
+  const int ncol = nw + 4 * fq;               // fp32 layout: this lane's first column in tile j = 0
+  const int pcol = nw + 16 * (fq & 1) + 8 * (fq >> 1);  // paired bf16 layout
+  float4_t bias[RN];
 #pragma unroll
-  for (int v = 0; v < NV; ++v)
-    bias[v] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)(a.bias + n + 4 * v) : float4_t{0.f, 0.f, 0.f, 0.f};
-  float4_t res[2][NP][NV];
-  auto load_res = [&](int i, float4_t (&dst)[NP][NV]) {
+  for (int j = 0; j < RN; ++j)
+    bias[j] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)(a.bias + ncol + 16 * j) : float4_t{0.f, 0.f, 0.f, 0.f};
+  float4_t res[2][RN];
+  auto load_res = [&](int i, float4_t (&dst)[RN]) {
+    const float* src = a.res + (size_t)out_row(min(mw + 16 * i + fr, a.M - 1)) * a.ldr + ncol;
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int m = mw + i * 16 + p * RPP + rsub;
-      const float* src = a.res + (size_t)out_row(min(m, a.M - 1)) * a.ldr + n;
-#pragma unroll
-      for (int v = 0; v < NV; ++v) dst[p][v] = *(const float4_t*)(src + 4 * v);
-    }
+    for (int j = 0; j < RN; ++j) dst[j] = *(const float4_t*)(src + 16 * j);
   };
   if (epi & AACLIP_EPI_RESID) load_res(0, res[0]);
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ep[(fq * 4 + e) * EP_LD + j * 16 + fr] = acc[i][j][e];
     if ((epi & AACLIP_EPI_RESID) && i + 1 < RM) load_res(i + 1, res[(i + 1) & 1]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float4_t v[RN];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int r = p * RPP + rsub;
-      const int m = mw + i * 16 + r;
-      float4_t v[NV];
+    for (int j = 0; j < RN; ++j) {
+      v[j] = acc[i][j] + bias[j];
+      if (epi & AACLIP_EPI_GELU)
 #pragma unroll
-      for (int q = 0; q < NV; ++q) {
-        v[q] = *(const float4_t*)(ep + r * EP_LD + col + 4 * q) + bias[q];
-        if (epi & AACLIP_EPI_GELU)
+        for (int t = 0; t < 4; ++t) v[j][t] = gelu_fast(v[j][t]);
+      if (epi & AACLIP_EPI_LEAKY)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) v[q][t] = gelu_fast(v[q][t]);
-        if (epi & AACLIP_EPI_LEAKY)
+        for (int t = 0; t < 4; ++t) v[j][t] = v[j][t] >= 0.f ? v[j][t] : 0.01f * v[j][t];
+      if (epi & AACLIP_EPI_RESID) v[j] += res[i & 1][j];
+    }
+    if (a.dbg & 2) {  // diagnostic: everything but the global stores
 #pragma unroll
-          for (int t = 0; t < 4; ++t) v[q][t] = v[q][t] >= 0.f ? v[q][t] : 0.01f * v[q][t];
-        if (epi & AACLIP_EPI_RESID) v[q] += res[i & 1][p][q];
+      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(v[j]));
+      continue;
+    }
+    const int m = mw + 16 * i + fr;
+    const size_t orow = (size_t)out_row(min(m, a.M - 1));
+    uint4 pk[RN / 2];
+    if (BF16OUT || (epi & AACLIP_EPI_AUX_BF16)) {
+#pragma unroll
+      for (int q = 0; q < RN / 2; ++q) pk[q] = pair_bf16(v[2 * q], v[2 * q + 1], fq);
+    }
+    if (m < a.M) {
+      if constexpr (BF16OUT) {
+#pragma unroll
+        for (int q = 0; q < RN / 2; ++q) *(uint4*)((uint16_t*)a.C + orow * a.ldc + pcol + 32 * q) = pk[q];
+      } else {
+#pragma unroll
+        for (int j = 0; j < RN; ++j) *(float4_t*)((float*)a.C + orow * a.ldc + ncol + 16 * j) = v[j];
       }
-      if (full || m < a.M) {
-        const size_t orow = (size_t)out_row(m);
-        if constexpr (BF16OUT) {
-          *(uint4*)((uint16_t*)a.C + orow * a.ldc + n) =
-              uint4{pack_bf16x2(v[0][0], v[0][1]), pack_bf16x2(v[0][2], v[0][3]),
-                    pack_bf16x2(v[1][0], v[1][1]), pack_bf16x2(v[1][2], v[1][3])};
-        } else {
+      if (epi & AACLIP_EPI_AUX_BF16) {
 #pragma unroll
-          for (int q = 0; q < NV; ++q) *(float4_t*)((float*)a.C + orow * a.ldc + n + 4 * q) = v[q];
-        }
-        if (epi & AACLIP_EPI_AUX_BF16) {
-#pragma unroll
-          for (int q = 0; q < NV; ++q)
-            *(uint2*)((uint16_t*)a.aux + orow * a.ldaux + n + 4 * q) =
-                uint2{pack_bf16x2(v[q][0], v[q][1]), pack_bf16x2(v[q][2], v[q][3])};
-        }
+        for (int q = 0; q < RN / 2; ++q) *(uint4*)((uint16_t*)a.aux + orow * a.ldaux + pcol + 32 * q) = pk[q];
       }
     }
   }
@@ -284,7 +280,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
         const bf16x8_t af = *(const bf16x8_t*)(base + a_off[i][kk]);
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);  // C^T tile
       }
     }
     if (a.setprio) __builtin_amdgcn_s_setprio(0);
@@ -298,14 +294,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
       for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  // The main loop's last barrier freed the LDS tiles: each wave stages through
-  // its own slot, no workgroup barrier needed.
-  float* ep = (float*)smem + wid * 16 * EP_LD;
   const int mw = m0 + wm * TM, nw = n0 + wn * TN;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
 #define EPI_CASE(BF, E)                                                \
   if (bf16_out == (BF) && key == (E)) {                                \
-    wave_epilogue<RM, RN, BF, E>(a, acc, ep, mw, nw, lane);            \
+    wave_epilogue<RM, RN, BF, E>(a, acc, mw, nw, lane);            \
     return;                                                            \
   }
   // the combinations the visual/text engines issue (engine.py)
@@ -319,9 +312,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   EPI_CASE(false, EPI_REMAP)                                             // patch embedding
 #undef EPI_CASE
   if (bf16_out)
-    wave_epilogue<RM, RN, true, -1>(a, acc, ep, mw, nw, lane);
+    wave_epilogue<RM, RN, true, -1>(a, acc, mw, nw, lane);
   else
-    wave_epilogue<RM, RN, false, -1>(a, acc, ep, mw, nw, lane);
+    wave_epilogue<RM, RN, false, -1>(a, acc, mw, nw, lane);
 }
 
 // ============================================================== fp32 MFMA kernel
@@ -409,13 +402,13 @@ int g_dbg = 0;
 
 extern "C" int aaclip_set_gemm_variant(int variant) {
   // bits 0-3: tile family (0 default, 1 = 256x256, 2 = 256x128); bits 4-7: tile-order
-  // group height (0 = 8); bit 8: setprio around the MFMA cluster; bit 9: skip epilogue
+  // group height (0 = 8); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 1024 || fam > 2) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 2048 || fam > 2) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 8;
   g_setprio = (variant >> 8) & 1;
-  g_dbg = (variant >> 9) & 1;
+  g_dbg = (variant >> 9) & 3;  // bit 9 skip epilogue, bit 10 skip the global stores
   return AACLIP_OK;
 }
 

@@ -54,6 +54,27 @@ def test_gemm_bf16_variants(dev, variant, M, N, K):
     assert (out.double() - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
 
 
+@pytest.mark.parametrize("gelu", [False, True])
+@pytest.mark.parametrize("M,N", [(18464, 3072), (18464, 4096), (577 * 3, 512), (100, 256)])
+def test_gemm_bf16_out_epilogue(dev, gelu, M, N):
+    """bf16-output epilogue (QKV: bias; c_fc: bias + GELU) at the C2 shapes and ragged
+    small ones: rows leave straight from the accumulators (C^T tile, lane = one row x 4
+    columns, permlane16-paired into 16-B stores); float64 reference."""
+    K = 1024
+    torch.manual_seed(M + N + gelu)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device=dev) * 0.5
+    out = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, w, out, bias=bias, gelu=gelu)
+    ref = a.double() @ w.double().T + bias.double()
+    if gelu:
+        ref = torch.nn.functional.gelu(ref)
+    err = (out.double() - ref).abs()
+    assert not torch.isnan(out).any()
+    assert (err <= 8e-3 * ref.abs() + 2e-3).all(), err.max().item()
+
+
 def test_gemm_bf16_asymmetric_identity(dev):
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     M = N = K = 256
