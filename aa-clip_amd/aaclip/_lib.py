@@ -30,6 +30,8 @@ SIGNATURES = {
     "aaclip_abi_version": [],
     "aaclip_arch": [],
     "aaclip_gemm": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _I, _P, _P, _L, _P, _L, _I, _I, _I, _P],
+    "aaclip_gemm_fp8": [_I, _I, _I, _I, _P, _L, _P, _P, _L, _P, _P, _L, _I, _P, _P, _L, _P, _L, _I, _I, _I, _P],
+    "aaclip_quant_fp8_rows": [_I, _P, _L, _P, _L, _P, _I, _I, _P],
     "aaclip_set_gemm_variant": [_I],
     "aaclip_attention": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "aaclip_im2col": [_I, _P, _P, _I, _I, _I, _I, _I, _P],

@@ -45,11 +45,27 @@ def _proj_weight(ad: dict, prefix: str):
     return ad[prefix + ".fc.weight"], False
 
 
+FP8 = ops.FP8
+
+
+def _quant_weight_fp8(w: torch.Tensor):
+    """Per-output-channel e4m3 weights: scale[n] = max|W[n]|/448, W8 = RNE(W/scale)."""
+    w = w.detach().float()
+    s = (w.abs().amax(dim=1) / 448.0).clamp_min(1e-30)
+    return (w / s[:, None]).to(FP8).contiguous(), s.contiguous()
+
+
 class VisualEngine:
     def __init__(self, vparams: dict, adapter: dict, *, levels=(6, 12, 18, 24), image_adapt_until=6,
                  image_adapt_weight=0.1, dtype=torch.bfloat16):
-        if dtype not in (torch.bfloat16, torch.float32):
-            raise ValueError("dtype must be bfloat16 or float32")
+        """dtype: bfloat16 (perf path), float32 (parity mode) or float8_e4m3fn (config C5:
+        the four block GEMMs per layer run on e4m3 weights (per-output-channel scales) and
+        per-token e4m3 activations through the K=128 fp8 MFMA; everything else is bf16)."""
+        if dtype not in (torch.bfloat16, torch.float32, FP8):
+            raise ValueError("dtype must be bfloat16, float32 or float8_e4m3fn")
+        self.fp8 = dtype == FP8
+        if self.fp8:
+            dtype = torch.bfloat16
         self.dtype = dtype
         self.levels = list(levels)
         self.adapt_until = int(image_adapt_until)
@@ -81,6 +97,10 @@ class VisualEngine:
                 w_fc=cdt(vparams[p + "mlp.c_fc.weight"]), b_fc=f32(vparams[p + "mlp.c_fc.bias"]),
                 w_pr=cdt(vparams[p + "mlp.c_proj.weight"]), b_pr=f32(vparams[p + "mlp.c_proj.bias"]),
             ))
+        if self.fp8:  # e4m3 copies of the block GEMM weights (the bf16 copies are dropped)
+            for blk in self.blocks:
+                for k in ("w_qkv", "w_o", "w_fc", "w_pr"):
+                    blk[k] = _quant_weight_fp8(blk[k])
         self.w_adapt = [cdt(adapter[f"layer_adapters.{i}.fc.0.weight"]) for i in range(self.adapt_until)]
         self.w_seg, relus = [], []
         for i in range(len(self.levels)):
@@ -121,6 +141,9 @@ class VisualEngine:
             # patch cosine by ~1e-4 (x100 in the map) — the largest single bf16
             # term in the anomaly-map error budget, for ~15 us per batch of 32.
             segbuf=e(B * P, (L + 1) * EMBED, dt=torch.float32),
+            # fp8 mode: e4m3 activation rows + per-row scales feeding the fp8 GEMMs
+            q8=e(R, 4 * WIDTH, dt=FP8) if self.fp8 else None,
+            qs=e(R, dt=torch.float32) if self.fp8 else None,
             grid=e(B * P, dt=torch.float32), partial=e(B * ((P + 63) // 64) * EMBED, dt=torch.float32),
             det=e(B, EMBED, dt=torch.float32), score=e(B, dt=torch.float32),
             map=e(B, S, S, dt=torch.float32),
@@ -147,16 +170,25 @@ class VisualEngine:
         ops.embed_ln(X, self.cls, self.pos, self.ln_pre, self.blocks[0]["ln1"], H, B, n_tok)
         lvl = {lv: j for j, lv in enumerate(self.levels)}
         last = self.levels[-1]
+        if self.fp8:
+            q8, qs = ws["q8"], ws["qs"]
+
+            def lin(a, w, out, **kw):  # e4m3 rows of a (per-row scale), then the fp8 GEMM
+                q = q8.view(-1)[:a.numel()].view(a.shape)
+                ops.quant_fp8_rows(a, q, qs)
+                ops.gemm_fp8(q, qs, w[0], w[1], out, **kw)
+        else:
+            lin = ops.gemm
         for i in range(last):
             blk = self.blocks[i]
-            ops.gemm(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
+            lin(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
             ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS)
-            ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
+            lin(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
             ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], H)
-            ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True)
+            lin(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True)
             adapt = i < self.adapt_until
-            ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X,
-                     aux=ws["xb"] if (adapt and ws["xb"] is not None) else None)
+            lin(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X,
+                aux=ws["xb"] if (adapt and ws["xb"] is not None) else None)
             tap = ws["taps"][lvl[i + 1]] if (i + 1) in lvl else None
             nxt = self.blocks[i + 1]["ln1"] if i + 1 < last else None
             u = None

@@ -63,6 +63,56 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
     rows_out = M if row_group == 0 else ((M - 1) // row_group) * row_group_out + row_offset + (M - 1) % row_group + 1
     if out.shape[0] < rows_out or (row_group and M % row_group):
         raise ValueError("gemm output rows too small for the row remap")
+    epi, ldr, ldaux = _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux)
+    call("aaclip_gemm", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w), w.stride(0),
+         _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
+         row_group, row_group_out, row_offset, _stream())
+    return out
+
+
+FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), one byte per element
+
+
+def quant_fp8_rows(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor) -> None:
+    """Per-row e4m3 quantisation: scale[r] = max|x[r]|/448, q = RNE(x/scale)."""
+    _dev(x, q, scale)
+    _rowmajor(x, "x")
+    _rowmajor(q, "q")
+    if q.dtype != FP8 or scale.dtype != torch.float32 or not scale.is_contiguous():
+        raise TypeError("q must be float8_e4m3fn and scale contiguous fp32")
+    rows, cols = x.shape
+    if tuple(q.shape) != (rows, cols) or scale.numel() < rows:
+        raise ValueError("quant_fp8_rows shape mismatch")
+    call("aaclip_quant_fp8_rows", dtag(x), _ptr(x), x.stride(0), _ptr(q), q.stride(0), _ptr(scale), rows, cols,
+         _stream())
+
+
+def gemm_fp8(a: torch.Tensor, a_scale: torch.Tensor, w: torch.Tensor, w_scale: torch.Tensor, out: torch.Tensor, *,
+             bias=None, gelu=False, leaky=False, residual=None, aux=None, row_group=0, row_group_out=0,
+             row_offset=0) -> torch.Tensor:
+    """out = epilogue(a_scale[:,None] * w_scale[None,:] * (a @ w.T)) with e4m3 a [M,K], w [N,K]."""
+    _dev(a, a_scale, w, w_scale, out, bias, residual, aux)
+    for t, n in ((a, "a"), (w, "w"), (out, "out")):
+        _rowmajor(t, n)
+    if a.dtype != FP8 or w.dtype != FP8:
+        raise TypeError("gemm_fp8 operands must be float8_e4m3fn")
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K or out.shape[1] != N or a_scale.numel() < M or w_scale.numel() != N:
+        raise ValueError(f"gemm_fp8 shape mismatch a{tuple(a.shape)} w{tuple(w.shape)} out{tuple(out.shape)}")
+    if a_scale.dtype != torch.float32 or w_scale.dtype != torch.float32:
+        raise TypeError("fp8 scales must be fp32")
+    rows_out = M if row_group == 0 else ((M - 1) // row_group) * row_group_out + row_offset + (M - 1) % row_group + 1
+    if out.shape[0] < rows_out or (row_group and M % row_group):
+        raise ValueError("gemm output rows too small for the row remap")
+    epi, ldr, ldaux = _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux)
+    call("aaclip_gemm_fp8", dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(a_scale), _ptr(w), w.stride(0),
+         _ptr(w_scale), _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
+         row_group, row_group_out, row_offset, _stream())
+    return out
+
+
+def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux):
     epi = 0
     if bias is not None:
         if bias.dtype != torch.float32 or bias.numel() != N:
@@ -86,10 +136,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
             raise ValueError("aux must be bf16 [rows, N]")
         epi |= _lib.EPI_AUX_BF16
         ldaux = aux.stride(0)
-    call("aaclip_gemm", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w), w.stride(0),
-         _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
-         row_group, row_group_out, row_offset, _stream())
-    return out
+    return epi, ldr, ldaux
 
 
 # ------------------------------------------------------------------------ attention

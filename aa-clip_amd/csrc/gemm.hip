@@ -40,6 +40,8 @@ struct GemmArgs {
   int group_m;   // tile-order group height (L2 reuse), default 8
   int setprio;   // raise wave priority around the MFMA cluster
   int dbg;       // diagnostic: 1 = skip the epilogue (accumulators kept live)
+  const float* a_scale;  // fp8 only: per-row scale of A (dequant = q * a_scale[m])
+  const float* w_scale;  // fp8 only: per-output-channel scale of W
 };
 
 __device__ __forceinline__ int remap_row(const GemmArgs& a, int m) {
@@ -119,7 +121,7 @@ __device__ __forceinline__ uint4 pair_bf16(const float4_t& lo, const float4_t& h
 
 // EPI >= 0: compile-time epilogue flags (AACLIP_EPI_* | EPI_REMAP) so each used
 // combination is straight-line code; EPI = -1: flags read at run time (any combination).
-template <int RM, int RN, bool BF16OUT, int EPI>
+template <int RM, int RN, bool BF16OUT, int EPI, bool SCALED>
 __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
                                               int lane) {
   static_assert(RN % 2 == 0, "column tiles are paired");
@@ -132,6 +134,11 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
 #pragma unroll
   for (int j = 0; j < RN; ++j)
     bias[j] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)(a.bias + ncol + 16 * j) : float4_t{0.f, 0.f, 0.f, 0.f};
+  float4_t wsc[RN];  // fp8: per-column weight scales of this lane's 4 columns in tile j
+  if constexpr (SCALED) {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) wsc[j] = *(const float4_t*)(a.w_scale + ncol + 16 * j);
+  }
   float4_t res[2][RN];
   auto load_res = [&](int i, float4_t (&dst)[RN]) {
     const float* src = a.res + (size_t)out_row(min(mw + 16 * i + fr, a.M - 1)) * a.ldr + ncol;
@@ -143,9 +150,14 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
   for (int i = 0; i < RM; ++i) {
     if ((epi & AACLIP_EPI_RESID) && i + 1 < RM) load_res(i + 1, res[(i + 1) & 1]);
     float4_t v[RN];
+    float asc = 1.f;
+    if constexpr (SCALED) asc = a.a_scale[min(mw + 16 * i + fr, a.M - 1)];
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
-      v[j] = acc[i][j] + bias[j];
+      if constexpr (SCALED)
+        v[j] = acc[i][j] * (wsc[j] * asc) + bias[j];
+      else
+        v[j] = acc[i][j] + bias[j];
       if (epi & AACLIP_EPI_GELU)
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[j][t] = gelu_fast(v[j][t]);
@@ -182,14 +194,23 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
   }
 }
 
-// ============================================================== bf16 MFMA kernel
-template <int BM, int BN, int WM, int WN>
+// ==================================================== bf16 / fp8 MFMA kernel
+// FP8: A and W are OCP e4m3 bytes with a per-row (A) and per-output-channel (W)
+// fp32 scale folded into the epilogue; the main loop runs the block-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 with unit (e8m0 127) block scales -- the
+// K=128 form runs at 2x the bf16 MFMA rate. The LDS image is the same 128-byte
+// row per K-step (64 bf16 or 128 fp8 elements), so staging is shared; a lane's
+// fp8 fragment is 32 consecutive K bytes = two swizzled 16-B chunks.
+typedef __attribute__((ext_vector_type(8))) int i32x8_t;
+
+template <int BM, int BN, int WM, int WN, bool FP8 = false>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   constexpr int NWAVES = WM * WN;
-  constexpr int BK = 64;
+  constexpr int ES = FP8 ? 1 : 2;  // element bytes
+  constexpr int BK = 128 / ES;     // K elements per stage (128 bytes per row)
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int RM = TM / 16, RN = TN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int A_LOADS = A_BYTES / (NWAVES * 1024);  // glds per wave per tile
   constexpr int B_LOADS = B_BYTES / (NWAVES * 1024);
@@ -205,31 +226,31 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const uint16_t* __restrict__ Ag = (const uint16_t*)a.A;
-  const uint16_t* __restrict__ Wg = (const uint16_t*)a.W;
+  const char* __restrict__ Ag = (const char*)a.A;
+  const char* __restrict__ Wg = (const char*)a.W;
 
   // Per-lane source pointers for the DMA pieces (row r = piece*8 + lane/8,
-  // physical chunk p = lane%8 holds logical chunk p ^ (r&7)).
-  const uint16_t* a_src[A_LOADS];
-  const uint16_t* b_src[B_LOADS];
+  // physical 16-B chunk p = lane%8 holds logical chunk p ^ (r&7)).
+  const char* a_src[A_LOADS];
+  const char* b_src[B_LOADS];
 #pragma unroll
   for (int i = 0; i < A_LOADS; ++i) {
     const int r = (i * NWAVES + wid) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (r & 7);
     const int gr = min(m0 + r, a.M - 1);
-    a_src[i] = Ag + (size_t)gr * a.lda + c * 8;
+    a_src[i] = Ag + ((size_t)gr * a.lda) * ES + c * 16;
   }
 #pragma unroll
   for (int i = 0; i < B_LOADS; ++i) {
     const int r = (i * NWAVES + wid) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (r & 7);
-    b_src[i] = Wg + (size_t)(n0 + r) * a.ldw + c * 8;
+    b_src[i] = Wg + ((size_t)(n0 + r) * a.ldw) * ES + c * 16;
   }
 
 #define GEMM_STAGE(kt, buf)                                                                  \
   do {                                                                                       \
     char* base_ = smem + (buf) * STAGE_BYTES;                                                \
-    const int koff_ = (kt) * BK;                                                             \
+    const int koff_ = (kt) * 128;                                                            \
     _Pragma("unroll") for (int i = 0; i < A_LOADS; ++i)                                      \
       __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + koff_),                      \
                                        LDS_PTR(base_ + (i * NWAVES + wid) * 1024), 16, 0, 0); \
@@ -246,20 +267,23 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-  // fragment read offsets (bytes within a stage), kk = 0/1 half of BK
+  // fragment read offsets (bytes within a stage). bf16: kk = 0/1 half of the
+  // 64-element K-step, chunk kk*4 + fq. fp8: the lane's 32-byte fragment of the
+  // 128-element K-step, chunks 2fq and 2fq + 1 (kk = 0/1).
   const int fr = lane & 15, fq = lane >> 4;
+  auto chunk = [&](int kk) { return FP8 ? 2 * fq + kk : kk * 4 + fq; };
   int a_off[RM][2], b_off[RN][2];
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
     const int r = wm * TM + i * 16 + fr;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) a_off[i][kk] = r * 128 + (((kk * 4 + fq) ^ (r & 7)) << 4);
+    for (int kk = 0; kk < 2; ++kk) a_off[i][kk] = r * 128 + ((chunk(kk) ^ (r & 7)) << 4);
   }
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
     const int r = wn * TN + j * 16 + fr;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) b_off[j][kk] = A_BYTES + r * 128 + (((kk * 4 + fq) ^ (r & 7)) << 4);
+    for (int kk = 0; kk < 2; ++kk) b_off[j][kk] = A_BYTES + r * 128 + ((chunk(kk) ^ (r & 7)) << 4);
   }
 
   const int nk = a.K / BK;
@@ -270,17 +294,34 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
     if (kt + 1 < nk) GEMM_STAGE(kt + 1, cur ^ 1);
     const char* base = smem + cur * STAGE_BYTES;
     if (a.setprio) __builtin_amdgcn_s_setprio(1);
+    if constexpr (FP8) {
+      i32x8_t bf[RN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8_t bf[RN];
-#pragma unroll
-      for (int j = 0; j < RN; ++j) bf[j] = *(const bf16x8_t*)(base + b_off[j][kk]);
+      for (int j = 0; j < RN; ++j) {
+        const int4 lo = *(const int4*)(base + b_off[j][0]), hi = *(const int4*)(base + b_off[j][1]);
+        bf[j] = i32x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      }
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
-        const bf16x8_t af = *(const bf16x8_t*)(base + a_off[i][kk]);
+        const int4 lo = *(const int4*)(base + a_off[i][0]), hi = *(const int4*)(base + a_off[i][1]);
+        const i32x8_t af = i32x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);  // C^T tile
+        for (int j = 0; j < RN; ++j)  // formats 0/0 = e4m3/e4m3, block scales 2^0
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af, acc[i][j], 0, 0, 0, 127, 0, 127);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8_t bf[RN];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bf[j] = *(const bf16x8_t*)(base + b_off[j][kk]);
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+          const bf16x8_t af = *(const bf16x8_t*)(base + a_off[i][kk]);
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);  // C^T tile
+        }
       }
     }
     if (a.setprio) __builtin_amdgcn_s_setprio(0);
@@ -298,7 +339,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
 #define EPI_CASE(BF, E)                                                \
   if (bf16_out == (BF) && key == (E)) {                                \
-    wave_epilogue<RM, RN, BF, E>(a, acc, mw, nw, lane);            \
+    wave_epilogue<RM, RN, BF, E, FP8>(a, acc, mw, nw, lane);       \
     return;                                                            \
   }
   // the combinations the visual/text engines issue (engine.py)
@@ -312,9 +353,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   EPI_CASE(false, EPI_REMAP)                                             // patch embedding
 #undef EPI_CASE
   if (bf16_out)
-    wave_epilogue<RM, RN, true, -1>(a, acc, mw, nw, lane);
+    wave_epilogue<RM, RN, true, -1, FP8>(a, acc, mw, nw, lane);
   else
-    wave_epilogue<RM, RN, false, -1>(a, acc, mw, nw, lane);
+    wave_epilogue<RM, RN, false, -1, FP8>(a, acc, mw, nw, lane);
 }
 
 // ============================================================== fp32 MFMA kernel
@@ -374,20 +415,20 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
     }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool FP8 = false>
 int launch_bf16(GemmArgs a, hipStream_t s) {
   if (a.N % BN) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, BM);
   a.tiles_n = a.N / BN;
-  const size_t lds = 2 * (size_t)(BM + BN) * 64 * 2;
+  const size_t lds = 2 * (size_t)(BM + BN) * 128;
   static bool attr_set = false;  // benign race: idempotent attribute write
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN>,
+    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, FP8>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return AACLIP_ERR_LAUNCH;
     attr_set = true;
   }
-  gemm_bf16_kernel<BM, BN, WM, WN><<<a.tiles_m * a.tiles_n, WM * WN * 64, lds, s>>>(a);
+  gemm_bf16_kernel<BM, BN, WM, WN, FP8><<<a.tiles_m * a.tiles_n, WM * WN * 64, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -429,7 +470,8 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
   AACLIP_REQUIRE(row_group >= 0 && (row_group == 0 || row_group_out >= row_group));
   if (M == 0) return AACLIP_OK;
   GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
-             out_dtype, row_group, row_group_out, row_offset, 0, 0, g_group_m, g_setprio, g_dbg};
+             out_dtype, row_group, row_group_out, row_offset, 0, 0, g_group_m, g_setprio, g_dbg,
+             nullptr, nullptr};
   hipStream_t s = (hipStream_t)stream;
   if (in_dtype == AACLIP_BF16) {
     AACLIP_REQUIRE(K % 64 == 0 && N % 128 == 0);
@@ -450,4 +492,28 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
   gemm_f32_kernel<<<a.tiles_m * a.tiles_n, 256, 0, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
+}
+
+extern "C" int aaclip_gemm_fp8(int out_dtype, int M, int N, int K, const void* A, int64_t lda,
+                               const float* a_scale, const void* W, int64_t ldw, const float* w_scale,
+                               void* C, int64_t ldc, int epilogue, const float* bias, const float* residual,
+                               int64_t ldr, void* aux, int64_t ldaux, int row_group, int row_group_out,
+                               int row_offset, void* stream) {
+  AACLIP_REQUIRE(out_dtype == AACLIP_F32 || out_dtype == AACLIP_BF16);
+  AACLIP_REQUIRE(A && W && C && a_scale && w_scale && M >= 0 && N > 0 && K > 0);
+  AACLIP_REQUIRE(K % 128 == 0 && N % 128 == 0);
+  AACLIP_REQUIRE(lda >= K && ldw >= K && ldc >= N && lda % 16 == 0 && ldw % 16 == 0 && ldc % 4 == 0);
+  AACLIP_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0 && ((uintptr_t)C % 16) == 0);
+  AACLIP_REQUIRE(((uintptr_t)w_scale % 16) == 0);
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_BIAS) || (bias && ((uintptr_t)bias % 16) == 0));
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_RESID) || (residual && ldr >= N && ldr % 4 == 0));
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_AUX_BF16) || (aux && ldaux >= N && ldaux % 4 == 0));
+  AACLIP_REQUIRE(row_group >= 0 && (row_group == 0 || row_group_out >= row_group));
+  if (M == 0) return AACLIP_OK;
+  GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
+             out_dtype, row_group, row_group_out, row_offset, 0, 0, g_group_m, g_setprio, 0,
+             a_scale, w_scale};
+  hipStream_t s = (hipStream_t)stream;
+  if (N % 256 == 0) return launch_bf16<256, 256, 2, 4, true>(a, s);  // 320x256 spills with 8-VGPR fp8 fragments
+  return launch_bf16<256, 128, 4, 2, true>(a, s);
 }

@@ -316,6 +316,60 @@ __global__ __launch_bounds__(256) void im2col_kernel(int out_dtype, const float*
 
 inline bool dtype_ok(int d) { return d == AACLIP_F32 || d == AACLIP_BF16; }
 
+
+// ------------------------------------------------------------------ fp8 quantisation
+// Per-row symmetric quantisation to OCP e4m3 for the fp8 GEMM (config C5):
+// scale[row] = max|x[row]| / 448 (448 = largest finite e4m3), q = RNE(x / scale)
+// via v_cvt_pk_fp8_f32. One wave per row; lane l owns elements 8l + 512c .. +7,
+// so each pass moves 16-B (bf16) / 32-B (fp32) contiguous pieces.
+__device__ __forceinline__ void load8(const void* p, int dtype, size_t off, float (&v)[8]) {
+  if (dtype == AACLIP_F32) {
+    const float4_t a = *(const float4_t*)((const float*)p + off), b = *(const float4_t*)((const float*)p + off + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = a[j];
+      v[4 + j] = b[j];
+    }
+  } else {
+    const uint4 r = *(const uint4*)((const uint16_t*)p + off);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void quant_fp8_kernel(int in_dtype, const void* __restrict__ x, int64_t ldx,
+                                                        uint8_t* __restrict__ q, int64_t ldq,
+                                                        float* __restrict__ scale, int rows, int cols) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float amax = 0.f;
+  for (int c0 = 8 * lane; c0 < cols; c0 += 512) {
+    float v[8];
+    load8(x, in_dtype, (size_t)row * ldx + c0, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+  }
+  amax = wave_max(amax);
+  const float sc = amax > 0.f ? amax * (1.0f / 448.0f) : 1.0f;
+  const float inv = amax > 0.f ? 448.0f / amax : 1.0f;
+  if (lane == 0) scale[row] = sc;
+  for (int c0 = 8 * lane; c0 < cols; c0 += 512) {
+    float v[8];
+    load8(x, in_dtype, (size_t)row * ldx + c0, v);
+    uint32_t w0 = 0, w1 = 0;
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, w0, false);
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, w0, true);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, w1, false);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, w1, true);
+    *(uint2*)(q + (size_t)row * ldq + c0) = uint2{w0, w1};
+  }
+}
+
 }  // namespace
 
 extern "C" int aaclip_embed_ln(int out_dtype, float* x, const float* cls, const float* pos,
@@ -407,6 +461,18 @@ extern "C" int aaclip_im2col(int out_dtype, const float* img, void* cols, int ba
   const size_t total = (size_t)batch * g * g * (k_padded / 8);
   im2col_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
       out_dtype, img, cols, batch, channels, img_size, patch, g, k_padded);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int64_t ldq, float* scale,
+                                     int rows, int cols, void* stream) {
+  AACLIP_REQUIRE(dtype_ok(in_dtype) && x && q && scale && rows >= 0 && cols > 0 && cols % 8 == 0);
+  AACLIP_REQUIRE(ldx >= cols && ldq >= cols && ldx % 8 == 0 && ldq % 8 == 0);
+  AACLIP_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)q % 8) == 0);
+  if (rows == 0) return AACLIP_OK;
+  quant_fp8_kernel<<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(in_dtype, x, ldx, (uint8_t*)q, ldq, scale,
+                                                                        rows, cols);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

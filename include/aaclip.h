@@ -67,6 +67,31 @@ int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K,
                 int row_group, int row_group_out, int row_offset, void* stream);
 
 /*
+ * fp8 GEMM (config C5: fp8 MFMA weights):
+ *   C[M,N] = epilogue( a_scale[m] * w_scale[n] * (A8[M,K] . W8[N,K]^T) )
+ * A8, W8: OCP e4m3 bytes (gfx950 FP8), per-row / per-output-channel fp32 scales
+ * (dequantised value = byte * scale). The main loop runs the block-scaled
+ * K=128 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales) at twice the
+ * bf16 rate; the scales fold into the epilogue ahead of bias/activation/residual.
+ * Same epilogue flags and row remap as aaclip_gemm. K % 128 == 0, N % 128 == 0,
+ * lda/ldw multiples of 16 bytes, w_scale 16-B aligned.
+ * Replaces: the same nn.Linear call sites as aaclip_gemm, at reduced precision.
+ */
+int aaclip_gemm_fp8(int out_dtype, int M, int N, int K, const void* A, int64_t lda,
+                    const float* a_scale, const void* W, int64_t ldw, const float* w_scale,
+                    void* C, int64_t ldc, int epilogue, const float* bias,
+                    const float* residual, int64_t ldr, void* aux, int64_t ldaux,
+                    int row_group, int row_group_out, int row_offset, void* stream);
+
+/*
+ * Per-row fp8 quantisation for aaclip_gemm_fp8's A operand:
+ *   scale[r] = max_c |x[r,c]| / 448 (1 for an all-zero row); q[r,c] = e4m3(x[r,c] / scale[r])
+ * (round-to-nearest-even, v_cvt_pk_fp8_f32). x: fp32 or bf16 [rows, cols], cols % 8 == 0.
+ */
+int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int64_t ldq,
+                          float* scale, int rows, int cols, void* stream);
+
+/*
  * Tuning hook: select the bf16 GEMM tile family for benchmarking. Bits 0-3:
  * 0 = default dispatch (320x256 when N % 256 == 0, else 256x128),
  * 1 = 256x256 (N % 256 == 0), 2 = 256x128; bits 4-7:

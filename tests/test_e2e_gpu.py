@@ -99,9 +99,12 @@ def test_text_anchor_parity(dev, golden, weights, dtype):
             np.testing.assert_allclose(T, tx[f"{cls}_T_{key}"], atol=t_tol, rtol=t_tol * 10)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float8_e4m3fn])
 def test_c5_shapes_parity(dev, golden, dtype):
-    """448 px (1025 tokens), 6 levels, relu projections: map vs the reference's golden."""
+    """448 px (1025 tokens), 6 levels, relu projections: map vs the reference's golden.
+    float8_e4m3fn = config C5's fp8 MFMA mode (block GEMMs on e4m3 weights/activations):
+    held to a documented looser bound, since e4m3 (3 mantissa bits) cannot meet the fp32
+    contract; its measured error is printed."""
     import os
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_c5.npz"))
     lv = tuple(int(v) for v in g["levels"])
@@ -121,8 +124,16 @@ def test_c5_shapes_parity(dev, golden, dtype):
         seg, det = eng.forward(x)
         grid = np.stack([(100.0 * (f @ T)).cpu().numpy() for f in seg], axis=1)
         np.testing.assert_allclose(grid, g["grid_A"], atol=5e-3)
-    else:
+    elif dtype == torch.bfloat16:
         assert (err <= 3e-3 + 1.5e-2 * np.abs(ref)).all()
+    else:
+        rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+        within = np.mean(err <= 1e-3 + 1e-2 * np.abs(ref))
+        print(f"fp8 c5: map rel-L2 {rel:.3e}, frac within fp32 contract {within:.4f}, "
+              f"score err {np.abs(score.cpu().numpy() - g['score']).max():.2e}")
+        assert rel < 0.05
+        np.testing.assert_allclose(score.cpu().numpy(), g["score"], atol=2e-2)
+        return
     np.testing.assert_allclose(score.cpu().numpy(), g["score"], atol=1e-3)
 
 

@@ -1,0 +1,129 @@
+"""fp8 path of config C5 ("fp8 MFMA weights", BASELINE.json configs[4]) on the MI355X:
+per-row e4m3 quantisation (aaclip_quant_fp8_rows) and the K=128 block-scaled MFMA
+GEMM (aaclip_gemm_fp8) against float64 references on the dequantised operands.
+The fp8 GEMM is exact products + fp32 accumulation of e4m3 values, so it is
+checked tightly against float64 on the SAME quantised operands; the end-to-end fp8
+error against the fp32 reference path is reported by tests/test_e2e_gpu.py."""
+import pytest
+import torch
+
+from aaclip import ops
+
+pytestmark = pytest.mark.gpu
+FP8 = torch.float8_e4m3fn
+
+
+def _quant_ref(x):
+    xf = x.float()
+    amax = xf.abs().amax(dim=1)
+    scale = torch.where(amax > 0, amax * (1.0 / 448.0), torch.ones_like(amax))
+    inv = torch.where(amax > 0, 448.0 / amax, torch.ones_like(amax))
+    return (xf * inv[:, None]).to(FP8), scale
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,cols", [(1, 8), (37, 1024), (577, 4096), (1000, 768)])
+def test_quant_fp8_rows(dev, dtype, rows, cols):
+    torch.manual_seed(rows + cols)
+    x = (torch.randn(rows, cols, device=dev) * torch.logspace(-3, 3, rows, device=dev)[:, None]).to(dtype)
+    x[0, :] = 0 if rows > 1 else x[0, :]
+    q = torch.empty(rows, cols, device=dev, dtype=FP8)
+    s = torch.empty(rows, device=dev)
+    ops.quant_fp8_rows(x, q, s)
+    q_ref, s_ref = _quant_ref(x)
+    assert torch.equal(s, s_ref)
+    # v_cvt_pk_fp8_f32 vs torch's cast: identical except rare one-code differences
+    # (measured <= 0.1 % of elements, normal-range rounding ties): allow adjacent codes only
+    qi, ri = q.view(torch.uint8).int(), q_ref.view(torch.uint8).int()
+    diff = qi != ri
+    assert diff.float().mean().item() < 5e-3
+    assert ((qi - ri).abs()[diff] <= 1).all()
+    deq = q.float() * s[:, None]
+    err = (deq - x.float()).abs()
+    assert (err <= 2.0 ** -4 * x.float().abs() + s[:, None] * 2.0 ** -9).all()
+
+
+def _wq(w):
+    """Per-output-channel weight quantisation (what the engine does at load time)."""
+    amax = w.abs().amax(dim=1).clamp_min(1e-30)
+    s = amax / 448.0
+    return (w / s[:, None]).to(FP8), s.float().contiguous()
+
+
+@pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (4100, 4096, 1024),
+                                   (300, 256, 128)])
+def test_gemm_fp8_plain(dev, M, N, K):
+    torch.manual_seed(M * 3 + N + K)
+    a = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) * K ** -0.5
+    a8 = torch.empty(M, K, device=dev, dtype=FP8)
+    sa = torch.empty(M, device=dev)
+    ops.quant_fp8_rows(a, a8, sa)
+    w8, sw = _wq(w)
+    out = torch.empty(M, N, device=dev)
+    ops.gemm_fp8(a8, sa, w8, sw, out)
+    ref = (a8.double() * sa.double()[:, None]) @ (w8.double() * sw.double()[:, None]).T
+    scale = (a8.double().abs() * sa.double()[:, None]) @ (w8.double().abs() * sw.double()[:, None]).T
+    err = (out.double() - ref).abs()
+    # MFMA fp8 products are exact; its internal K=128 reduction is not a strict fp32
+    # fmaf chain (measured <= 1.4e-5 of sum|a*b|)
+    assert (err <= 3e-5 * scale + 1e-6).all(), (err / scale).max().item()
+    # and the fp8 product approximates the unquantised one at e4m3 precision
+    full = a.double() @ w.double().T
+    rel = ((out.double() - full).norm() / full.norm()).item()
+    assert rel < 0.05, rel
+
+
+def test_gemm_fp8_identity_asymmetric(dev):
+    """A = I with an asymmetric B (small integers, exact in e4m3) pins the operand/accumulator layout."""
+    M = N = K = 256
+    a8 = torch.eye(M, K, device=dev).to(FP8)
+    w = (torch.arange(N * K, device=dev, dtype=torch.float32).reshape(N, K) % 13) - 6
+    w8 = w.to(FP8)
+    ones_m = torch.ones(M, device=dev)
+    ones_n = torch.ones(N, device=dev)
+    out = torch.empty(M, N, device=dev)
+    ops.gemm_fp8(a8, ones_m, w8, ones_n, out)
+    torch.testing.assert_close(out, w.T.contiguous(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("case", ["bias_gelu_bf16", "bias_resid_aux", "leaky", "remap"])
+def test_gemm_fp8_epilogues(dev, case):
+    torch.manual_seed(7)
+    M, N, K = 20 * 577, 1024, 1024
+    a = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) * K ** -0.5
+    a8 = torch.empty(M, K, device=dev, dtype=FP8)
+    sa = torch.empty(M, device=dev)
+    ops.quant_fp8_rows(a, a8, sa)
+    w8, sw = _wq(w)
+    bias = torch.randn(N, device=dev) * 0.1
+    y = (a8.double() * sa.double()[:, None]) @ (w8.double() * sw.double()[:, None]).T
+    tol = 3e-5 * ((a8.double().abs() * sa.double()[:, None]) @ (w8.double().abs() * sw.double()[:, None]).T) + 1e-6
+    if case == "bias_gelu_bf16":
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm_fp8(a8, sa, w8, sw, out, bias=bias, gelu=True)
+        ref = torch.nn.functional.gelu(y + bias.double())
+        assert ((out.double() - ref).abs() <= 8e-3 * ref.abs() + 2e-3).all()
+    elif case == "bias_resid_aux":
+        x = torch.randn(M, N, device=dev)
+        x0 = x.clone()
+        aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm_fp8(a8, sa, w8, sw, x, bias=bias, residual=x, aux=aux)
+        ref = y + bias.double() + x0.double()
+        assert ((x.double() - ref).abs() <= tol + 1e-6 * ref.abs()).all()
+        assert ((aux.double() - ref).abs() <= 8e-3 * ref.abs() + 1e-3).all()
+    elif case == "leaky":
+        out = torch.empty(M, N, device=dev)
+        ops.gemm_fp8(a8, sa, w8, sw, out, leaky=True)
+        ref = torch.nn.functional.leaky_relu(y, 0.01)
+        assert ((out.double() - ref).abs() <= tol).all()
+    else:  # patch rows -> token rows after a CLS slot (patch embedding)
+        P = 577 - 1
+        Mp = 20 * P
+        out = torch.zeros(20 * 577, N, device=dev)
+        ops.gemm_fp8(a8[:Mp], sa[:Mp], w8, sw, out, row_group=P, row_group_out=577, row_offset=1)
+        ref = y[:Mp].view(20, P, N)
+        got = out.view(20, 577, N)
+        assert (got[:, 0] == 0).all()
+        assert ((got[:, 1:].double() - ref).abs() <= tol[:Mp].view(20, P, N)).all()

@@ -54,8 +54,8 @@ def test_tokenizer_matches_reference(golden):
         normal, abnormal = _sentences(real)
         assert np.array_equal(tokenize(normal).numpy(), t[f"{cls}_tok_normal"])
         assert np.array_equal(tokenize(abnormal).numpy(), t[f"{cls}_tok_abnormal"])
-    with pytest.raises(KeyError):
-        tokenize(["a sentence outside the prompt ensemble"])
+    # outside the prompt ensemble the BPE restatement tokenises (pinned by tests/test_bpe.py)
+    assert tokenize(["a sentence outside the prompt ensemble"])[0, 0] == 49406
 
 
 def test_prompt_table_covers_every_class():

@@ -38,11 +38,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--shapes", default="qkv,out,fc,proj,adapter", help="GEMM shapes to run")
     ap.add_argument("--map", action="store_true", help="also run the anomaly-map stream kernel (C2 sizes)")
+    ap.add_argument("--fp8", action="store_true", help="also time the fp8 GEMM (+ the row quantisation of A)")
+    ap.add_argument("--tokens", type=int, default=577, help="tokens per image (577 @336 px, 1025 @448 px)")
     ap.add_argument("--torch", action="store_true",
                     help="also time torch (hipBLASLt) on the same GEMM shapes, for comparison only")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    B, n, W = args.batch, 577, 1024
+    B, n, W = args.batch, args.tokens, 1024
     R = B * n
     g = torch.Generator(device=dev).manual_seed(0)
     rnd = lambda *s, std=1.0: (torch.randn(*s, device=dev, generator=g) * std)  # noqa: E731
@@ -75,6 +77,21 @@ def main():
                     if prev is None or ms < prev[0]:
                         res[key] = (ms, 2.0 * R * N * K / ms / 1e9)
         _lib.call("aaclip_set_gemm_variant", 0)
+        if args.fp8:
+            FP8 = torch.float8_e4m3fn
+            for name, (N, K, kw, a, w, bias, out) in data.items():
+                a8 = torch.empty(R, K, device=dev, dtype=FP8)
+                sa = torch.empty(R, device=dev)
+                ops.quant_fp8_rows(a, a8, sa)
+                sw = (w.float().abs().amax(1) / 448).contiguous()
+                w8 = (w.float() / sw[:, None]).to(FP8)
+                f = lambda: ops.gemm_fp8(a8, sa, w8, sw, out, bias=bias if kw.get("bias") else None,  # noqa: E731
+                                         gelu=kw.get("gelu", False), leaky=kw.get("leaky", False),
+                                         residual=out if kw.get("resid") else None)
+                ms = timeit(f, args.reps)
+                res[f"{name}/fp8"] = (ms, 2.0 * R * N * K / ms / 1e9)
+                ms = timeit(lambda: ops.quant_fp8_rows(a, a8, sa), args.reps)
+                res[f"{name}/quantA"] = (ms, R * K * 3 / ms / 1e9)
         if args.torch:  # library comparison: linear (+bias) -> epilogue in torch ops
             F = torch.nn.functional
             for name, (N, K, kw, a, w, bias, out) in data.items():
@@ -110,7 +127,7 @@ def main():
         ms = timeit(lambda: ops.layernorm(x, lw, lb, h), args.reps)
         res["layernorm"] = (ms, (R * W * 6) / ms / 1e6)
     for k, (ms, rate) in res.items():
-        unit = "GB/s" if k in ("layernorm", "patch_scores") else "TFLOP/s"
+        unit = "GB/s" if k in ("layernorm", "patch_scores") or k.endswith("quantA") else "TFLOP/s"
         print(f"{k:10s} {ms * 1e3:9.1f} us  {rate:8.1f} {unit}")
 
 
