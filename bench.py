@@ -50,15 +50,16 @@ def pmc_traffic(key):
 HBM_PEAK_GBS = 8000.0      # HBM3E spec peak
 
 
-def synthetic_visual_weights(dev, seed=111, n_levels=4, adapt_until=6):
-    """Random-init ViT-L/14-336 + adapters, generated on device (reference key names)."""
+def synthetic_visual_weights(dev, seed=111, n_levels=4, adapt_until=6, n_tok=577):
+    """Random-init ViT-L/14 (+ adapters), generated on device (reference key names);
+    n_tok = 577 at 336 px, 1025 at 448 px (config C5)."""
     g = torch.Generator(device=dev).manual_seed(seed)
     r = lambda *s, std=1.0: torch.randn(*s, device=dev, generator=g) * std  # noqa: E731
     W = WIDTH
     vp = {
         "visual.conv1.weight": r(W, 3, 14, 14, std=588 ** -0.5),
         "visual.class_embedding": r(W, std=W ** -0.5),
-        "visual.positional_embedding": r(577, W, std=W ** -0.5),
+        "visual.positional_embedding": r(n_tok, W, std=W ** -0.5),
         "visual.ln_pre.weight": 1 + r(W, std=0.1), "visual.ln_pre.bias": r(W, std=0.05),
         "visual.ln_post.weight": 1 + r(W, std=0.1), "visual.ln_post.bias": r(W, std=0.05),
     }
@@ -159,6 +160,62 @@ def roofline_map(eng, ws, T, reps=50):
             "blur_upsample_GBs": round(B * S * S * 4 / (t_bu * 1e-3) / 1e9, 1)}
 
 
+def c5_leg(dev, steps: int, warmup: int, streams: int, batch: int = 32):
+    """Config C5 (BASELINE.json configs[4]): 448 px (1025 tokens), 6 feature levels,
+    block GEMMs on fp8 (e4m3 weights + per-token e4m3 activations, K=128 MFMA), batch
+    of 32 on one GPU; the same workload in bf16 beside it. Accuracy of the fp8 mode:
+    its anomaly maps against the fp32 parity mode of this path (itself pinned to the
+    reference's C5 golden within 1e-5) on 2 of the images."""
+    S, lv = 448, (4, 8, 12, 16, 20, 24)
+    vp, ad = synthetic_visual_weights(dev, seed=448, n_levels=len(lv), n_tok=(S // 14) ** 2 + 1)
+    g = torch.Generator(device=dev).manual_seed(448)
+    x = torch.randn(batch, 3, S, S, device=dev, generator=g)
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
+    out = {"workload": "C5: 448x448 (32x32 patch grid, 1025 tokens), 6 levels, batch 32, 1 GPU",
+           "gflop_per_image": round(flops_per_image(1025, levels=6) / 1e9, 2)}
+    maps = {}
+    for tag, dt in (("fp8", ops.FP8), ("bf16", torch.bfloat16)):
+        eng = VisualEngine(vp, ad, levels=lv, dtype=dt)
+        run = eng.graphed_predict(batch, S, "Medical", streams=streams)
+        for _ in range(warmup):
+            run(x, T)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run(x, T)
+        torch.cuda.synchronize()
+        dt_s = time.perf_counter() - t0
+        out[tag] = {"images_per_sec": round(batch * steps / dt_s, 2), "ms_per_step": round(dt_s / steps * 1e3, 3)}
+        maps[tag] = eng.predict(x[:2], T, "Medical")[0].clone()
+        if tag == "fp8":  # the fp8 GEMM roofline (QKV + c_fc shapes at this size)
+            ws = eng._workspace(batch, S)
+            blk, R = eng.blocks[0], ws["x"].shape[0]
+            q8, qs = ws["q8"].view(-1)[:R * WIDTH].view(R, WIDTH), ws["qs"]
+            ops.quant_fp8_rows(ws["h"], q8, qs)
+            st = torch.cuda.current_stream()
+            t_q = time_launches(lambda: ops.gemm_fp8(q8, qs, *blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"]), 10, st)
+            t_f = time_launches(lambda: ops.gemm_fp8(q8, qs, *blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True),
+                                10, st)
+            t_qa = time_launches(lambda: ops.quant_fp8_rows(ws["h"], q8, qs), 10, st)
+            fl = 2.0 * R * WIDTH * 7 * WIDTH / 2
+            ach = fl / ((t_q + t_f) / 2 * 1e-3) / 1e12
+            out["fp8_gemm_roofline"] = {"kernel": "gemm_bf16_kernel<256,256,2,4,FP8> (QKV + c_fc launches)",
+                                        "bound": "mfma", "unit": "TFLOP/s", "achieved": round(ach, 1),
+                                        "peak": 2 * BF16_PEAK_TFLOPS, "frac": round(ach / (2 * BF16_PEAK_TFLOPS), 4),
+                                        "avg_launch_us": round((t_q + t_f) / 2 * 1e3, 2),
+                                        "quant_rows_us": round(t_qa * 1e3, 2)}
+        del eng, run
+        torch.cuda.empty_cache()
+    eng = VisualEngine(vp, ad, levels=lv, dtype=torch.float32)
+    ref = eng.predict(x[:2], T, "Medical")[0]
+    for tag in ("fp8", "bf16"):
+        d = maps[tag] - ref
+        out[tag]["map_rel_l2_vs_fp32"] = float(d.norm() / ref.norm())
+        out[tag]["map_max_abs_err_vs_fp32"] = float(d.abs().max())
+        out[tag]["frac_pixels_within_fp32_contract"] = float((d.abs() <= 1e-3 + 1e-2 * ref.abs()).float().mean())
+    return out
+
+
 def cpu_baseline_and_parity(n_images: int, dev, streams: int):
     """CPU leg on rank 0: the numpy oracle (fp32 restatement of the reference,
     pinned to its golden vectors) timed on this host's cores over a bounded
@@ -223,6 +280,7 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="concurrent image chunks per GPU (HIP streams)")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-C5 leg (448 px, 6 levels, fp8)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -302,6 +360,10 @@ def main():
         line["roofline_map"] = roofline_map(eng, ws, T)
     if rank == 0 and world == 1 and args.cpu_images > 0:
         line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(args.cpu_images, dev, args.streams)
+    if rank == 0 and world == 1 and not args.no_c5:
+        del eng, run
+        torch.cuda.empty_cache()
+        line["c5"] = c5_leg(dev, max(3, args.steps // 2), args.warmup, args.streams)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
