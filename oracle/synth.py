@@ -159,3 +159,36 @@ def state_checksum(sd: dict[str, np.ndarray]) -> str:
         h.update(k.encode())
         h.update(np.ascontiguousarray(sd[k], dtype=np.float32).tobytes())
     return h.hexdigest()
+
+
+_OPENAI_FP16 = ("conv1.weight", "in_proj_weight", "in_proj_bias", "out_proj.weight", "out_proj.bias",
+                "c_fc.weight", "c_fc.bias", "c_proj.weight", "c_proj.bias", "visual.proj", "text_projection")
+
+
+def write_openai_checkpoint(path: str, seed: int = 111) -> None:
+    """A synthetic checkpoint in the OpenAI ViT-L-14-336px.pt state-dict layout: the
+    tensors OpenAI's convert_weights casts (reference model/model.py:265-286) stored as
+    fp16, the rest fp32, plus the input_resolution/context_length/vocab_size entries the
+    loaders drop (reference model/model.py:366). Plain torch.save (no pickled code)."""
+    import torch
+    sd = clip_state_dict(seed)
+    out = {}
+    for k, v in sd.items():
+        t = torch.from_numpy(np.ascontiguousarray(v))
+        out[k] = t.half() if k.endswith(_OPENAI_FP16) else t
+    out["input_resolution"] = torch.tensor(336)
+    out["context_length"] = torch.tensor(CONTEXT)
+    out["vocab_size"] = torch.tensor(VOCAB)
+    torch.save(out, path)
+
+
+def torch_state_checksum(sd) -> str:
+    """SHA-256 over a torch state dict's floating tensors as float32 (sorted keys)."""
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        v = sd[k]
+        if not v.is_floating_point():
+            continue
+        h.update(k.encode())
+        h.update(v.detach().float().contiguous().cpu().numpy().tobytes())
+    return h.hexdigest()
