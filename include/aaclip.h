@@ -96,7 +96,8 @@ int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int
  * 0 = default dispatch (320x256 when N % 256 == 0, else 256x128),
  * 1 = 256x256 (N % 256 == 0), 2 = 256x128; bits 4-7:
  * tile-order group height (0 = 8); bit 8: s_setprio around the MFMA cluster;
- * bit 9: diagnostic timing mode that skips the epilogue (outputs NOT written).
+ * bit 9: diagnostic timing mode that skips the epilogue (outputs NOT written);
+ * bit 10: diagnostic mode that runs the epilogue but skips its global stores.
  * Process-global; not for production use.
  */
 int aaclip_set_gemm_variant(int variant);
