@@ -415,6 +415,190 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
     }
 }
 
+// ================================ 8-phase ping-pong bf16 kernel (256x256x64)
+// The K-step is cut into 4 phases, one per C quadrant of the wave tile (64x32 =
+// 4x2 MFMA tiles x 2 k-halves = 16 MFMAs). Each phase: ds_read the quadrant's
+// register subtile, issue ONE 16-KiB LDS region of a later K-step (2 LDS-DMA per
+// thread), counted vmcnt, barrier, MFMA cluster, barrier. The two wave rows are
+// staggered by one barrier, so on every SIMD one wave runs its MFMA cluster while
+// the other issues its LDS reads and DMA (ping-pong). LDS per stage = 4 regions of
+// 128 rows x 128 B grouped by the phase that first reads them:
+//   A0 = rows {0..63, 128..191} (A sub-block 0 of both wave rows), A1 = the other
+//   rows, B0 / B1 = the first / second 32 W-rows of every wave column.
+// Phase reads: P1 A0+B0, P2 B1, P3 A1, P4 -- and issues (K-step k): P1 B1(k+1),
+// P2 A1(k+1), P3 A0(k+2), P4 B0(k+2): every region is rewritten >= 2 phases after
+// its last read (WAR) and lands 5-6 phases before it is read; each phase's
+// vmcnt(8) (4 regions of 2 DMAs in flight) retires the region the next phase
+// reads (RAW: read one phase after the wait, past both groups' barriers).
+// Loads past the last K-step re-read its columns into regions nobody reads again,
+// so the vmcnt arithmetic stays uniform. Operands via buffer descriptors (rows >= M
+// read as zero; outputs dropped by the epilogue's bound check).
+__global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
+  constexpr int BM = 256, BN = 256, TM = 128, TN = 64, RM = 8, RN = 4;
+  constexpr int REGION = 128 * 128;                 // bytes per LDS region
+  constexpr int STAGE = 4 * REGION;                 // A0, A1, B0, B1
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  int tm, tn;
+  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const auto ars = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)((uint32_t)a.M * (uint32_t)a.lda * 2u),
+                                                     0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, (int)((uint32_t)a.N * (uint32_t)a.ldw * 2u),
+                                                     0x00020000);
+  // DMA: thread t fills row t/8 of a 64-row piece, physical 16-B chunk t%8 holds
+  // logical chunk (t%8) ^ (row%8) (row%8 = (t/8)%8 in every piece)
+  const int prow = t >> 3;
+  const int pchunk = ((t & 7) ^ (prow & 7)) * 8;
+  const int a_vo = ((m0 + prow) * (int)a.lda + pchunk) * 2;
+  const int w_vo = ((n0 + ((prow >> 5) & 1) * 64 + (prow & 31)) * (int)a.ldw + pchunk) * 2;
+  const int a_row = (int)a.lda * 2, w_row = (int)a.ldw * 2;  // bytes per row
+  const int nk = a.K / 64;
+  // region r of K-step kt into stage kt&1 (r: 0 = A0, 1 = A1, 2 = B0, 3 = B1)
+  auto issue = [&](int r, int kt) {
+    const int kc = min(kt, nk - 1) * 128;  // phantom loads past the end re-read the last K-step
+    char* dst = smem + (kt & 1) * STAGE + r * REGION;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if (r < 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, LDS_PTR(dst + g * 8192 + wid * 1024), 16, a_vo,
+                                                 (g * 128 + r * 64) * a_row + kc, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + g * 8192 + wid * 1024), 16, w_vo,
+                                                 (g * 128 + (r - 2) * 32) * w_row + kc, 0, 0);
+    }
+  };
+  // fragment offsets inside a region: local row (A: wr*64 + 16i + fr, B: wc*32 + 16j + fr),
+  // 16-B chunk (kk*4 + fq) ^ (fr & 7)
+  int a_rd[2], b_rd[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int sw = ((kk * 4 + fq) ^ (fr & 7)) << 4;
+    a_rd[kk] = (wr * 64 + fr) * 128 + sw;
+    b_rd[kk] = 2 * REGION + (wc * 32 + fr) * 128 + sw;
+  }
+  float4_t acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t af[4][2], bfr[2][2][2];  // A sub-block (4 tiles x kk), B sub-blocks [q][j][kk]
+
+  // prologue: all of K-step 0, then A0 / B0 of K-step 1 (the steady state's P3/P4 of K-step -1)
+  issue(0, 0);
+  issue(2, 0);
+  issue(3, 0);
+  issue(1, 0);
+  issue(0, 1);
+  issue(2, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0(0), B0(0) landed
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: wave row 1 runs one barrier behind
+
+  auto mfma_q = [&](int qa, int qb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qa * 4 + i][qb * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[qb][j][kk], af[i][kk], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto read_a = [&](const char* st, int q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = *(const bf16x8_t*)(st + q * REGION + a_rd[kk] + i * 2048);
+  };
+  auto read_b = [&](const char* st, int q) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bfr[q][j][kk] = *(const bf16x8_t*)(st + q * REGION + b_rd[kk] + j * 2048);
+  };
+#define PH_SYNC_MFMA(QA, QB)                                 \
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");           \
+  __builtin_amdgcn_s_barrier();                              \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
+  __builtin_amdgcn_sched_barrier(0);                         \
+  mfma_q(QA, QB);                                            \
+  __builtin_amdgcn_sched_barrier(0);                         \
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * STAGE;
+    // P1: A0 x B0
+    read_b(st, 0);
+    read_a(st, 0);
+    issue(3, kt + 1);
+    PH_SYNC_MFMA(0, 0)
+    // P2: A0 x B1
+    read_b(st, 1);
+    issue(1, kt + 1);
+    PH_SYNC_MFMA(0, 1)
+    // P3: A1 x B1
+    read_a(st, 1);
+    issue(0, kt + 2);
+    PH_SYNC_MFMA(1, 1)
+    // P4: A1 x B0
+    issue(2, kt + 2);
+    PH_SYNC_MFMA(1, 0)
+  }
+#undef PH_SYNC_MFMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phantom loads drained before exit
+  if (wr == 0) __builtin_amdgcn_s_barrier();         // re-balance the stagger
+  if (a.dbg & 1) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  const int mw = m0 + wr * TM, nw = n0 + wc * TN;
+  const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
+  const bool bf16_out = a.out_dtype != AACLIP_F32;
+#define EPI_CASE(BF, E)                                            \
+  if (bf16_out == (BF) && key == (E)) {                            \
+    wave_epilogue<RM, RN, BF, E, false>(a, acc, mw, nw, lane);     \
+    return;                                                        \
+  }
+  EPI_CASE(true, AACLIP_EPI_BIAS)
+  EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)
+  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)
+  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)
+  EPI_CASE(false, AACLIP_EPI_LEAKY)
+#undef EPI_CASE
+  if (bf16_out)
+    wave_epilogue<RM, RN, true, -1, false>(a, acc, mw, nw, lane);
+  else
+    wave_epilogue<RM, RN, false, -1, false>(a, acc, mw, nw, lane);
+}
+
+int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
+  if (a.N % 256 || a.K % 64) return AACLIP_ERR_ARG;
+  a.tiles_m = ceil_div(a.M, 256);
+  a.tiles_n = a.N / 256;
+  const size_t lds = 2 * 4 * 128 * 128;
+  static bool attr_set = false;  // benign race: idempotent attribute write
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)gemm_bf16_8ph_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return AACLIP_ERR_LAUNCH;
+    attr_set = true;
+  }
+  gemm_bf16_8ph_kernel<<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
 template <int BM, int BN, int WM, int WN, bool FP8 = false>
 int launch_bf16(GemmArgs a, hipStream_t s) {
   if (a.N % BN) return AACLIP_ERR_ARG;
@@ -442,10 +626,10 @@ int g_dbg = 0;
 }  // namespace
 
 extern "C" int aaclip_set_gemm_variant(int variant) {
-  // bits 0-3: tile family (0 default, 1 = 256x256, 2 = 256x128); bits 4-7: tile-order
+  // bits 0-3: tile family (0 default, 1 = 256x256, 2 = 256x128, 3 = 256x256 8-phase ping-pong); bits 4-7: tile-order
   // group height (0 = 8); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 2048 || fam > 2) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 2048 || fam > 4) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 8;
   g_setprio = (variant >> 8) & 1;
@@ -478,6 +662,12 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
     switch (g_gemm_variant) {
       case 1: return launch_bf16<256, 256, 2, 4>(a, s);
       case 2: return launch_bf16<256, 128, 4, 2>(a, s);
+      case 3:
+      case 4:  // 8-phase for the wide GEMMs only (N >= 2048), 320x256 below
+        if (N % 256 == 0 && (g_gemm_variant == 3 || N >= 2048) && (int64_t)M * lda * 2 < (1ll << 31) &&
+            (int64_t)N * ldw * 2 < (1ll << 31))
+          return launch_bf16_8ph(a, s);
+        break;
       default: break;
     }
     // M = B*577 tiles badly by 256 (18464 = 72.1 x 256 at B=32: 3.42 waves of 256x256

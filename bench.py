@@ -281,6 +281,7 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="concurrent image chunks per GPU (HIP streams)")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-C5 leg (448 px, 6 levels, fp8)")
+    ap.add_argument("--gemm-variant", type=int, default=0, help="aaclip_set_gemm_variant value (A/B runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -292,6 +293,9 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    if args.gemm_variant:
+        from aaclip import _lib
+        _lib.call("aaclip_set_gemm_variant", args.gemm_variant)
     vp, ad = synthetic_visual_weights(dev)
     eng = VisualEngine(vp, ad, dtype=torch.bfloat16)
     del vp
