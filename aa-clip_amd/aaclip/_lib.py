@@ -14,6 +14,7 @@ ABI_VERSION = 1
 
 F32 = 0
 BF16 = 1
+FP8 = 2
 EPI_BIAS = 1
 EPI_GELU = 2
 EPI_LEAKY = 4
@@ -32,6 +33,8 @@ SIGNATURES = {
     "aaclip_gemm": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _I, _P, _P, _L, _P, _L, _I, _I, _I, _P],
     "aaclip_gemm_fp8": [_I, _I, _I, _I, _P, _L, _P, _P, _L, _P, _P, _L, _I, _P, _P, _L, _P, _L, _I, _I, _I, _P],
     "aaclip_quant_fp8_rows": [_I, _P, _L, _P, _L, _P, _I, _I, _P],
+    "aaclip_gemm_fp8mx": [_I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _P, _P, _L, _P, _L, _P, _L, _P],
+    "aaclip_quant_fp8_mx": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _P],
     "aaclip_set_gemm_variant": [_I],
     "aaclip_attention": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "aaclip_im2col": [_I, _P, _P, _I, _I, _I, _I, _I, _P],

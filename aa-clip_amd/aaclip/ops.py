@@ -112,6 +112,54 @@ def gemm_fp8(a: torch.Tensor, a_scale: torch.Tensor, w: torch.Tensor, w_scale: t
     return out
 
 
+def mx_scales(rows: int, cols: int, device, ld: int = None) -> torch.Tensor:
+    """e8m0 scale buffer of an MX fp8 tensor [rows, cols]: [cols/128, ld, 2] uint8
+    (one byte per (row, 64-column block); the two blocks of a 128-K step adjacent)."""
+    return torch.empty(cols // 128, ld or rows, 2, device=device, dtype=torch.uint8)
+
+
+def quant_fp8_mx(x: torch.Tensor, q: torch.Tensor, sc: torch.Tensor) -> None:
+    """MX fp8: q = e4m3(x * 2^-e), e8m0 e per (row, 64-column block) into sc [cols/128, ld, 2]."""
+    _dev(x, q, sc)
+    _rowmajor(x, "x")
+    _rowmajor(q, "q")
+    rows, cols = x.shape
+    if q.dtype != FP8 or sc.dtype != torch.uint8 or tuple(q.shape) != (rows, cols):
+        raise TypeError("q must be float8_e4m3fn [rows, cols], sc uint8")
+    if sc.dim() != 3 or sc.shape[0] != cols // 128 or sc.shape[1] < rows or sc.shape[2] != 2 or not sc.is_contiguous():
+        raise ValueError("sc must be contiguous uint8 [cols/128, ld >= rows, 2]")
+    call("aaclip_quant_fp8_mx", dtag(x), _ptr(x), x.stride(0), _ptr(q), q.stride(0), _ptr(sc), sc.shape[1],
+         rows, cols, _stream())
+
+
+def gemm_fp8mx(a: torch.Tensor, a_sc: torch.Tensor, w: torch.Tensor, w_scale: torch.Tensor, out: torch.Tensor, *,
+               out_sc=None, bias=None, gelu=False, leaky=False, residual=None, aux=None) -> torch.Tensor:
+    """out = epilogue(w_scale[None,:] * (MX-dequant(a) @ w.T)); a: e4m3 [M,K] with e8m0 block scales
+    a_sc [K/128, ld, 2]; out fp32 / bf16, or e4m3 (then out_sc receives its MX scales)."""
+    _dev(a, a_sc, w, w_scale, out, out_sc, bias, residual, aux)
+    for t, n in ((a, "a"), (w, "w"), (out, "out")):
+        _rowmajor(t, n)
+    if a.dtype != FP8 or w.dtype != FP8:
+        raise TypeError("gemm_fp8mx operands must be float8_e4m3fn")
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K or out.shape[1] != N or out.shape[0] < M or w_scale.numel() != N:
+        raise ValueError(f"gemm_fp8mx shape mismatch a{tuple(a.shape)} w{tuple(w.shape)} out{tuple(out.shape)}")
+    if a_sc.dtype != torch.uint8 or a_sc.dim() != 3 or a_sc.shape[0] != K // 128 or a_sc.shape[1] < M:
+        raise ValueError("a_sc must be uint8 [K/128, ld >= M, 2]")
+    if out.dtype == FP8:
+        if out_sc is None or out_sc.shape[0] != N // 128 or out_sc.shape[1] < M:
+            raise ValueError("fp8 output needs out_sc uint8 [N/128, ld >= M, 2]")
+        odt = _lib.FP8
+    else:
+        odt = dtag(out)
+    epi, ldr, ldaux = _epilogue_flags(N, M, bias, gelu, leaky, residual, aux)
+    call("aaclip_gemm_fp8mx", odt, M, N, K, _ptr(a), a.stride(0), _ptr(a_sc), a_sc.shape[1], _ptr(w), w.stride(0),
+         _ptr(w_scale), _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
+         _ptr(out_sc), 0 if out_sc is None else out_sc.shape[1], _stream())
+    return out
+
+
 def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux):
     epi = 0
     if bias is not None:

@@ -42,7 +42,48 @@ struct GemmArgs {
   int dbg;       // diagnostic: 1 = skip the epilogue (accumulators kept live)
   const float* a_scale;  // fp8 only: per-row scale of A (dequant = q * a_scale[m])
   const float* w_scale;  // fp8 only: per-output-channel scale of W
+  const uint8_t* a_mx;   // fp8 MX A operand: e8m0 scale per (row, 64-K block), [K/128][ld_amx][2]
+  int64_t ld_amx;
+  uint8_t* c_mx;         // fp8 MX output: e8m0 scale per (row, 64-column block), [N/128][ld_cmx][2]
+  int64_t ld_cmx;
 };
+
+// smallest e with amax * 2^-e <= 448 (largest finite e4m3): the e8m0 block scale
+__device__ __forceinline__ int mx_exp(float amax) {
+  if (!(amax > 0.f)) return 0;
+  int x;
+  (void)frexpf(amax, &x);  // amax = m * 2^x, m in [0.5, 1)
+  int e = x - 9;           // amax * 2^-e in [256, 512)
+  if (ldexpf(amax, -e) > 448.f) e += 1;
+  return max(min(e, 127), -126);
+}
+__device__ __forceinline__ float pow2i(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+
+// cross-lane max over the 4 lanes {c, c+16, c+32, c+48} (one row of the C^T tile)
+__device__ __forceinline__ float max_over_fq(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// 4x4 dword transpose across the lane groups fq = lane/16: on entry lane fq holds
+// d[j] = its 4 fp8 columns of column tile j; on exit it holds tile j = fq's 16
+// consecutive bytes (d[q] = the 4 columns of lane group q).
+__device__ __forceinline__ void transpose_fq(uint32_t (&d)[4]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    auto r = __builtin_amdgcn_permlane32_swap(d[j], d[j + 2], false, false);
+    d[j] = r[0];
+    d[j + 2] = r[1];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k += 2) {
+    auto r = __builtin_amdgcn_permlane16_swap(d[k], d[k + 1], false, false);
+    d[k] = r[0];
+    d[k + 1] = r[1];
+  }
+}
 
 __device__ __forceinline__ int remap_row(const GemmArgs& a, int m) {
   return a.row_group > 0 ? (m / a.row_group) * a.row_group_out + a.row_offset + (m % a.row_group) : m;
@@ -121,10 +162,17 @@ __device__ __forceinline__ uint4 pair_bf16(const float4_t& lo, const float4_t& h
 
 // EPI >= 0: compile-time epilogue flags (AACLIP_EPI_* | EPI_REMAP) so each used
 // combination is straight-line code; EPI = -1: flags read at run time (any combination).
-template <int RM, int RN, bool BF16OUT, int EPI, bool SCALED>
+// OUTM: 0 = fp32 C, 1 = bf16 C, 2 = fp8 e4m3 C with an e8m0 scale per (row, 64
+// columns) -- the wave's 64-column tile is one block: row max over the 4 lane
+// groups, power-of-two scale, RNE to e4m3, 4x4 lane-group transpose -> 16-B stores.
+// SCALED: 0 = none, 1 = a_scale[row] * w_scale[col] (fp8 per-row), 2 = w_scale[col]
+// only (fp8 MX: the activation block scales were applied by the MFMA).
+template <int RM, int RN, int OUTM, int EPI, int SCALED>
 __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
                                               int lane) {
   static_assert(RN % 2 == 0, "column tiles are paired");
+  static_assert(OUTM != 2 || RN == 4, "fp8 MX output: one 64-column block per wave");
+  constexpr bool BF16OUT = OUTM == 1;
   const int fr = lane & 15, fq = lane >> 4;
   const int epi = EPI >= 0 ? EPI : a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
   auto out_row = [&](int m) { return (epi & EPI_REMAP) ? remap_row(a, m) : m; };
@@ -151,11 +199,13 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
     if ((epi & AACLIP_EPI_RESID) && i + 1 < RM) load_res(i + 1, res[(i + 1) & 1]);
     float4_t v[RN];
     float asc = 1.f;
-    if constexpr (SCALED) asc = a.a_scale[min(mw + 16 * i + fr, a.M - 1)];
+    if constexpr (SCALED == 1) asc = a.a_scale[min(mw + 16 * i + fr, a.M - 1)];
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
-      if constexpr (SCALED)
+      if constexpr (SCALED == 1)
         v[j] = acc[i][j] * (wsc[j] * asc) + bias[j];
+      else if constexpr (SCALED == 2)
+        v[j] = acc[i][j] * wsc[j] + bias[j];
       else
         v[j] = acc[i][j] + bias[j];
       if (epi & AACLIP_EPI_GELU)
@@ -173,6 +223,28 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
     }
     const int m = mw + 16 * i + fr;
     const size_t orow = (size_t)out_row(min(m, a.M - 1));
+    if constexpr (OUTM == 2) {
+      float amax = 0.f;
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) amax = fmaxf(amax, fabsf(v[j][t]));
+      const int e = mx_exp(max_over_fq(amax));
+      const float inv = pow2i(-e);
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(v[j][0] * inv, v[j][1] * inv, 0, false);
+        d[j] = __builtin_amdgcn_cvt_pk_fp8_f32(v[j][2] * inv, v[j][3] * inv, w, true);
+      }
+      transpose_fq(d);
+      if (m < a.M) {
+        *(uint4*)((uint8_t*)a.C + orow * a.ldc + nw + 16 * fq) = uint4{d[0], d[1], d[2], d[3]};
+        const int blk = nw >> 6;
+        if (fq == 0) a.c_mx[((size_t)(blk >> 1) * a.ld_cmx + orow) * 2 + (blk & 1)] = (uint8_t)(e + 127);
+      }
+      continue;
+    }
     uint4 pk[RN / 2];
     if (BF16OUT || (epi & AACLIP_EPI_AUX_BF16)) {
 #pragma unroll
@@ -203,8 +275,12 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
 // fp8 fragment is 32 consecutive K bytes = two swizzled 16-B chunks.
 typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 
-template <int BM, int BN, int WM, int WN, bool FP8 = false>
+// Q: 0 = bf16, 1 = fp8 with per-row A scales (epilogue), 2 = fp8 MX: A carries an
+// e8m0 scale per (row, 64-K block) staged through LDS next to the tiles and applied
+// by the MFMA's B-operand scale (the A tile is the MFMA's second operand).
+template <int BM, int BN, int WM, int WN, int Q = 0>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
+  constexpr bool FP8 = Q != 0, MX = Q == 2;
   constexpr int NWAVES = WM * WN;
   constexpr int ES = FP8 ? 1 : 2;  // element bytes
   constexpr int BK = 128 / ES;     // K elements per stage (128 bytes per row)
@@ -247,8 +323,22 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
     b_src[i] = Wg + ((size_t)(n0 + r) * a.ldw) * ES + c * 16;
   }
 
+  // MX: the A tile's scales for K-step kt = BM rows x 2 bytes, contiguous in the
+  // [K/128][ld_amx][2] layout; BM/128 waves DMA one dword per lane
+  constexpr int SC_BYTES = BM * 2;
+  const auto srs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.a_mx, 0, MX ? (int)((a.K / 128) * a.ld_amx * 2) : 0, 0x00020000);
+  auto stage_scales = [&](int kt, int buf) {
+    if constexpr (MX) {
+      if (wid < SC_BYTES / 256)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, LDS_PTR(smem + 2 * STAGE_BYTES + buf * SC_BYTES + wid * 256), 4,
+                                                 (m0 * 2 + wid * 256 + lane * 4), (int)(kt * a.ld_amx * 2), 0, 0);
+    }
+  };
+
 #define GEMM_STAGE(kt, buf)                                                                  \
   do {                                                                                       \
+    stage_scales(kt, buf);                                                                   \
     char* base_ = smem + (buf) * STAGE_BYTES;                                                \
     const int koff_ = (kt) * 128;                                                            \
     _Pragma("unroll") for (int i = 0; i < A_LOADS; ++i)                                      \
@@ -267,11 +357,14 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-  // fragment read offsets (bytes within a stage). bf16: kk = 0/1 half of the
-  // 64-element K-step, chunk kk*4 + fq. fp8: the lane's 32-byte fragment of the
-  // 128-element K-step, chunks 2fq and 2fq + 1 (kk = 0/1).
+  // fragment read offsets (bytes within a stage): 16-B chunk kk*4 + fq of the row.
+  // bf16: kk = 0/1 half of the 64-element K-step. fp8: the lane's 32-byte fragment
+  // of the 128-element K-step is chunks fq and 4 + fq -- the K=128 MFMA takes a
+  // lane's bytes 0-15 as K 16fq.. and bytes 16-31 as K 64+16fq.. (probed with
+  // tools/mxprobe.py), so hardware 32-K block b is logical K 32b..32b+31 and the
+  // lane supplying its e8m0 scale (lane group b) owns exactly that range.
   const int fr = lane & 15, fq = lane >> 4;
-  auto chunk = [&](int kk) { return FP8 ? 2 * fq + kk : kk * 4 + fq; };
+  auto chunk = [&](int kk) { return kk * 4 + fq; };
   int a_off[RM][2], b_off[RN][2];
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
@@ -305,9 +398,12 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
       for (int i = 0; i < RM; ++i) {
         const int4 lo = *(const int4*)(base + a_off[i][0]), hi = *(const int4*)(base + a_off[i][1]);
         const i32x8_t af = i32x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        int sb = 127;  // e8m0 2^0
+        if constexpr (MX)  // this lane's A block: row wm*TM + 16i + fr, 64-block fq/2 of the K-step
+          sb = *(const uint8_t*)(smem + 2 * STAGE_BYTES + cur * SC_BYTES + (wm * TM + 16 * i + fr) * 2 + (fq >> 1));
 #pragma unroll
-        for (int j = 0; j < RN; ++j)  // formats 0/0 = e4m3/e4m3, block scales 2^0
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af, acc[i][j], 0, 0, 0, 127, 0, 127);
+        for (int j = 0; j < RN; ++j)  // formats 0/0 = e4m3/e4m3; W block scale 2^0, A block scale sb
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af, acc[i][j], 0, 0, 0, 127, 0, sb);
       }
     } else {
 #pragma unroll
@@ -337,25 +433,29 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   }
   const int mw = m0 + wm * TM, nw = n0 + wn * TN;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
-#define EPI_CASE(BF, E)                                                \
-  if (bf16_out == (BF) && key == (E)) {                                \
-    wave_epilogue<RM, RN, BF, E, FP8>(a, acc, mw, nw, lane);       \
+  constexpr int SC = Q == 1 ? 1 : (Q == 2 ? 2 : 0);
+  const int outm = a.out_dtype == AACLIP_F32 ? 0 : (a.out_dtype == AACLIP_BF16 ? 1 : 2);
+#define EPI_CASE(OM, E)                                                \
+  if (outm == (OM) && key == (E)) {                                    \
+    wave_epilogue<RM, RN, OM, E, SC>(a, acc, mw, nw, lane);            \
     return;                                                            \
   }
   // the combinations the visual/text engines issue (engine.py)
-  const bool bf16_out = a.out_dtype != AACLIP_F32;
-  EPI_CASE(true, AACLIP_EPI_BIAS)                                        // qkv
-  EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)                      // c_fc
-  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)                    // out-proj, c_proj
-  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)  // c_proj + bf16 copy
-  EPI_CASE(false, AACLIP_EPI_LEAKY)                                      // adapters, seg/det proj
-  EPI_CASE(false, 0)                                                     // seg/det proj (no relu)
-  EPI_CASE(false, EPI_REMAP)                                             // patch embedding
+  EPI_CASE(1, AACLIP_EPI_BIAS)                                        // qkv
+  EPI_CASE(1, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)                      // c_fc
+  EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)                     // out-proj, c_proj
+  EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)  // c_proj + bf16 copy
+  EPI_CASE(0, AACLIP_EPI_LEAKY)                                       // adapters, seg/det proj
+  EPI_CASE(0, 0)                                                      // seg/det proj (no relu)
+  EPI_CASE(0, EPI_REMAP)                                              // patch embedding
+  if constexpr (BN / WN == 64) {
+    EPI_CASE(2, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)                    // c_fc -> fp8 MX c_proj input
+  }
 #undef EPI_CASE
-  if (bf16_out)
-    wave_epilogue<RM, RN, true, -1, FP8>(a, acc, mw, nw, lane);
-  else
-    wave_epilogue<RM, RN, false, -1, FP8>(a, acc, mw, nw, lane);
+  if (outm == 1)
+    wave_epilogue<RM, RN, 1, -1, SC>(a, acc, mw, nw, lane);
+  else if (outm == 0)
+    wave_epilogue<RM, RN, 0, -1, SC>(a, acc, mw, nw, lane);
 }
 
 // ============================================================== fp32 MFMA kernel
@@ -567,7 +667,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   const bool bf16_out = a.out_dtype != AACLIP_F32;
 #define EPI_CASE(BF, E)                                            \
   if (bf16_out == (BF) && key == (E)) {                            \
-    wave_epilogue<RM, RN, BF, E, false>(a, acc, mw, nw, lane);     \
+    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0>(a, acc, mw, nw, lane); \
     return;                                                        \
   }
   EPI_CASE(true, AACLIP_EPI_BIAS)
@@ -577,9 +677,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   EPI_CASE(false, AACLIP_EPI_LEAKY)
 #undef EPI_CASE
   if (bf16_out)
-    wave_epilogue<RM, RN, true, -1, false>(a, acc, mw, nw, lane);
+    wave_epilogue<RM, RN, 1, -1, 0>(a, acc, mw, nw, lane);
   else
-    wave_epilogue<RM, RN, false, -1, false>(a, acc, mw, nw, lane);
+    wave_epilogue<RM, RN, 0, -1, 0>(a, acc, mw, nw, lane);
 }
 
 int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
@@ -599,20 +699,20 @@ int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   return AACLIP_OK;
 }
 
-template <int BM, int BN, int WM, int WN, bool FP8 = false>
+template <int BM, int BN, int WM, int WN, int Q = 0>
 int launch_bf16(GemmArgs a, hipStream_t s) {
   if (a.N % BN) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, BM);
   a.tiles_n = a.N / BN;
-  const size_t lds = 2 * (size_t)(BM + BN) * 128;
+  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (Q == 2 ? 2 * BM * 2 : 0);
   static bool attr_set = false;  // benign race: idempotent attribute write
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, FP8>,
+    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, Q>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return AACLIP_ERR_LAUNCH;
     attr_set = true;
   }
-  gemm_bf16_kernel<BM, BN, WM, WN, FP8><<<a.tiles_m * a.tiles_n, WM * WN * 64, lds, s>>>(a);
+  gemm_bf16_kernel<BM, BN, WM, WN, Q><<<a.tiles_m * a.tiles_n, WM * WN * 64, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -655,7 +755,7 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
   if (M == 0) return AACLIP_OK;
   GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
              out_dtype, row_group, row_group_out, row_offset, 0, 0, g_group_m, g_setprio, g_dbg,
-             nullptr, nullptr};
+             nullptr, nullptr, nullptr, 0, nullptr, 0};
   hipStream_t s = (hipStream_t)stream;
   if (in_dtype == AACLIP_BF16) {
     AACLIP_REQUIRE(K % 64 == 0 && N % 128 == 0);
@@ -702,8 +802,30 @@ extern "C" int aaclip_gemm_fp8(int out_dtype, int M, int N, int K, const void* A
   if (M == 0) return AACLIP_OK;
   GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
              out_dtype, row_group, row_group_out, row_offset, 0, 0, g_group_m, g_setprio, 0,
-             a_scale, w_scale};
+             a_scale, w_scale, nullptr, 0, nullptr, 0};
   hipStream_t s = (hipStream_t)stream;
-  if (N % 256 == 0) return launch_bf16<256, 256, 2, 4, true>(a, s);  // 320x256 spills with 8-VGPR fp8 fragments
-  return launch_bf16<256, 128, 4, 2, true>(a, s);
+  if (N % 256 == 0) return launch_bf16<256, 256, 2, 4, 1>(a, s);  // 320x256 spills with 8-VGPR fp8 fragments
+  return launch_bf16<256, 128, 4, 2, 1>(a, s);
+}
+
+extern "C" int aaclip_gemm_fp8mx(int out_dtype, int M, int N, int K, const void* A, int64_t lda, const void* a_mx,
+                                 int64_t ld_amx, const void* W, int64_t ldw, const float* w_scale, void* C,
+                                 int64_t ldc, int epilogue, const float* bias, const float* residual, int64_t ldr,
+                                 void* aux, int64_t ldaux, void* c_mx, int64_t ld_cmx, void* stream) {
+  AACLIP_REQUIRE(out_dtype == AACLIP_F32 || out_dtype == AACLIP_BF16 || out_dtype == AACLIP_FP8);
+  AACLIP_REQUIRE(A && W && C && a_mx && w_scale && M >= 0 && N > 0 && K > 0);
+  AACLIP_REQUIRE(K % 128 == 0 && N % 256 == 0 && ld_amx >= M);
+  AACLIP_REQUIRE(lda >= K && ldw >= K && ldc >= N && lda % 16 == 0 && ldw % 16 == 0 && ldc % 16 == 0);
+  AACLIP_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0 && ((uintptr_t)C % 16) == 0);
+  AACLIP_REQUIRE(((uintptr_t)w_scale % 16) == 0 && ((uintptr_t)a_mx % 4) == 0);
+  AACLIP_REQUIRE((int64_t)(K / 128) * ld_amx * 2 < (1ll << 31) && (int64_t)M * lda < (1ll << 31));
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_BIAS) || (bias && ((uintptr_t)bias % 16) == 0));
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_RESID) || (residual && ldr >= N && ldr % 4 == 0));
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_AUX_BF16) || (aux && ldaux >= N && ldaux % 4 == 0));
+  AACLIP_REQUIRE(out_dtype != AACLIP_FP8 || (c_mx && ld_cmx >= M && epilogue == (AACLIP_EPI_BIAS | AACLIP_EPI_GELU)));
+  if (M == 0) return AACLIP_OK;
+  GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
+             out_dtype, 0, 0, 0, 0, 0, g_group_m, g_setprio, 0,
+             nullptr, w_scale, (const uint8_t*)a_mx, ld_amx, (uint8_t*)c_mx, ld_cmx};
+  return launch_bf16<256, 256, 2, 4, 2>(a, (hipStream_t)stream);
 }

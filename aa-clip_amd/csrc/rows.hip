@@ -370,6 +370,47 @@ __global__ __launch_bounds__(256) void quant_fp8_kernel(int in_dtype, const void
   }
 }
 
+
+// MX variant: one wave per row, lane l owns elements 8l + 512c .. +7, so a 64-element
+// block is 8 consecutive lanes: max over them (3 xor-shuffles), power-of-two e8m0
+// scale, RNE to e4m3 after an exact 2^-e scaling.
+__device__ __forceinline__ int mx_exp_row(float amax) {
+  if (!(amax > 0.f)) return 0;
+  int x;
+  (void)frexpf(amax, &x);
+  int e = x - 9;
+  if (ldexpf(amax, -e) > 448.f) e += 1;
+  return max(min(e, 127), -126);
+}
+
+__global__ __launch_bounds__(256) void quant_mx_kernel(int in_dtype, const void* __restrict__ x, int64_t ldx,
+                                                       uint8_t* __restrict__ q, int64_t ldq,
+                                                       uint8_t* __restrict__ sc, int64_t ld_sc, int rows, int cols) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  for (int c0 = 8 * lane; c0 < cols; c0 += 512) {
+    float v[8];
+    load8(x, in_dtype, (size_t)row * ldx + c0, v);
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    const int e = mx_exp_row(amax);
+    const float inv = __uint_as_float((uint32_t)(127 - e) << 23);
+    uint32_t w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, 0, false);
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, w0, true);
+    uint32_t w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, 0, false);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, w1, true);
+    *(uint2*)(q + (size_t)row * ldq + c0) = uint2{w0, w1};
+    if ((lane & 7) == 0) {
+      const int blk = c0 >> 6;
+      sc[((size_t)(blk >> 1) * ld_sc + row) * 2 + (blk & 1)] = (uint8_t)(e + 127);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int aaclip_embed_ln(int out_dtype, float* x, const float* cls, const float* pos,
@@ -473,6 +514,18 @@ extern "C" int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, v
   if (rows == 0) return AACLIP_OK;
   quant_fp8_kernel<<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(in_dtype, x, ldx, (uint8_t*)q, ldq, scale,
                                                                         rows, cols);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_quant_fp8_mx(int in_dtype, const void* x, int64_t ldx, void* q, int64_t ldq, void* sc,
+                                   int64_t ld_sc, int rows, int cols, void* stream) {
+  AACLIP_REQUIRE(dtype_ok(in_dtype) && x && q && sc && rows >= 0 && cols > 0 && cols % 128 == 0);
+  AACLIP_REQUIRE(ldx >= cols && ldq >= cols && ldx % 8 == 0 && ldq % 8 == 0 && ld_sc >= rows);
+  AACLIP_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)q % 8) == 0);
+  if (rows == 0) return AACLIP_OK;
+  quant_mx_kernel<<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(in_dtype, x, ldx, (uint8_t*)q, ldq,
+                                                                       (uint8_t*)sc, ld_sc, rows, cols);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

@@ -187,23 +187,23 @@ def c5_leg(dev, steps: int, warmup: int, streams: int, batch: int = 32):
         dt_s = time.perf_counter() - t0
         out[tag] = {"images_per_sec": round(batch * steps / dt_s, 2), "ms_per_step": round(dt_s / steps * 1e3, 3)}
         maps[tag] = eng.predict(x[:2], T, "Medical")[0].clone()
-        if tag == "fp8":  # the fp8 GEMM roofline (QKV + c_fc shapes at this size)
+        if tag == "fp8":  # the fp8 MX GEMM roofline (QKV + c_fc shapes at this size)
             ws = eng._workspace(batch, S)
             blk, R = eng.blocks[0], ws["x"].shape[0]
-            q8, qs = ws["q8"].view(-1)[:R * WIDTH].view(R, WIDTH), ws["qs"]
-            ops.quant_fp8_rows(ws["h"], q8, qs)
+            a8, asc = ws["a8"], ws["asc"]
+            ops.quant_fp8_mx(ws["h"], a8, asc)
             st = torch.cuda.current_stream()
-            t_q = time_launches(lambda: ops.gemm_fp8(q8, qs, *blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"]), 10, st)
-            t_f = time_launches(lambda: ops.gemm_fp8(q8, qs, *blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True),
-                                10, st)
-            t_qa = time_launches(lambda: ops.quant_fp8_rows(ws["h"], q8, qs), 10, st)
+            t_q = time_launches(lambda: ops.gemm_fp8mx(a8, asc, *blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"]), 10, st)
+            t_f = time_launches(lambda: ops.gemm_fp8mx(a8, asc, *blk["w_fc"], ws["f8"], out_sc=ws["fsc"],
+                                                       bias=blk["b_fc"], gelu=True), 10, st)
+            t_qa = time_launches(lambda: ops.quant_fp8_mx(ws["h"], a8, asc), 10, st)
             fl = 2.0 * R * WIDTH * 7 * WIDTH / 2
             ach = fl / ((t_q + t_f) / 2 * 1e-3) / 1e12
-            out["fp8_gemm_roofline"] = {"kernel": "gemm_bf16_kernel<256,256,2,4,FP8> (QKV + c_fc launches)",
+            out["fp8_gemm_roofline"] = {"kernel": "gemm_bf16_kernel<256,256,2,4,MX> (QKV + c_fc launches)",
                                         "bound": "mfma", "unit": "TFLOP/s", "achieved": round(ach, 1),
                                         "peak": 2 * BF16_PEAK_TFLOPS, "frac": round(ach / (2 * BF16_PEAK_TFLOPS), 4),
                                         "avg_launch_us": round((t_q + t_f) / 2 * 1e3, 2),
-                                        "quant_rows_us": round(t_qa * 1e3, 2)}
+                                        "quant_mx_us": round(t_qa * 1e3, 2)}
         del eng, run
         torch.cuda.empty_cache()
     eng = VisualEngine(vp, ad, levels=lv, dtype=torch.float32)

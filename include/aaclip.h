@@ -33,6 +33,7 @@ extern "C" {
 
 #define AACLIP_F32 0
 #define AACLIP_BF16 1
+#define AACLIP_FP8 2   /* OCP e4m3 + e8m0 block scales (fp8 MX activations, config C5) */
 
 /* GEMM epilogue flags (applied in this order) */
 #define AACLIP_EPI_BIAS 1      /* + bias[n] (fp32)                          */
@@ -82,6 +83,31 @@ int aaclip_gemm_fp8(int out_dtype, int M, int N, int K, const void* A, int64_t l
                     void* C, int64_t ldc, int epilogue, const float* bias,
                     const float* residual, int64_t ldr, void* aux, int64_t ldaux,
                     int row_group, int row_group_out, int row_offset, void* stream);
+
+/*
+ * fp8 MX GEMM (config C5): C[M,N] = epilogue( w_scale[n] * sum_k A[m,k] 2^(a_mx[m,k/64]-127) W8[n,k] )
+ * A: e4m3 with an e8m0 scale per (row, 64-K block), stored [K/128][ld_amx][2] bytes
+ * (the two 64-blocks of one 128-K step adjacent); W8: e4m3 with fp32 per-output-
+ * channel scales. The block scales are applied by the MFMA itself
+ * (v_mfma_scale_f32_16x16x128_f8f6f4's per-lane B scale), staged through LDS.
+ * out_dtype AACLIP_FP8 (only with bias+GELU, the c_fc -> c_proj hand-off): C is
+ * written as e4m3 with its own e8m0 scale per (row, 64 columns) in c_mx
+ * [N/128][ld_cmx][2], ready to be the A operand of the next MX GEMM.
+ * K % 128 == 0, N % 256 == 0, ld_amx >= M.
+ */
+int aaclip_gemm_fp8mx(int out_dtype, int M, int N, int K, const void* A, int64_t lda,
+                      const void* a_mx, int64_t ld_amx, const void* W, int64_t ldw,
+                      const float* w_scale, void* C, int64_t ldc, int epilogue,
+                      const float* bias, const float* residual, int64_t ldr, void* aux,
+                      int64_t ldaux, void* c_mx, int64_t ld_cmx, void* stream);
+
+/*
+ * MX fp8 quantisation: q[r,c] = e4m3(x[r,c] * 2^-e), e = the smallest exponent with
+ * max|x[r, 64-block]| * 2^-e <= 448; sc[(c/128)*ld_sc + r][(c/64)%2] = e + 127.
+ * x: fp32 or bf16 [rows, cols], cols % 128 == 0.
+ */
+int aaclip_quant_fp8_mx(int in_dtype, const void* x, int64_t ldx, void* q, int64_t ldq, void* sc,
+                        int64_t ld_sc, int rows, int cols, void* stream);
 
 /*
  * Per-row fp8 quantisation for aaclip_gemm_fp8's A operand:

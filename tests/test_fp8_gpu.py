@@ -127,3 +127,82 @@ def test_gemm_fp8_epilogues(dev, case):
         got = out.view(20, 577, N)
         assert (got[:, 0] == 0).all()
         assert ((got[:, 1:].double() - ref).abs() <= tol[:Mp].view(20, P, N)).all()
+
+
+# ------------------------------------------------------------------ MX (block-scaled) fp8
+def _mx_dequant(q, sc):
+    """e4m3 [M,K] + e8m0 [K/128, ld, 2] -> float64 [M,K]."""
+    M, K = q.shape
+    e = sc[:, :M, :].permute(1, 0, 2).reshape(M, K // 64).double() - 127.0  # [M, K/64]
+    return q.double() * torch.pow(2.0, e).repeat_interleave(64, dim=1)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,cols", [(1, 128), (37, 1024), (577, 4096), (1000, 768)])
+def test_quant_fp8_mx(dev, dtype, rows, cols):
+    torch.manual_seed(rows * 7 + cols)
+    x = torch.randn(rows, cols, device=dev) * torch.logspace(-4, 4, cols // 64, device=dev).repeat_interleave(64)
+    x = x.to(dtype)
+    if rows > 1:
+        x[1, :64] = 0  # an all-zero block
+    q = torch.empty(rows, cols, device=dev, dtype=FP8)
+    sc = ops.mx_scales(rows, cols, dev, ld=rows + 3)
+    ops.quant_fp8_mx(x, q, sc)
+    deq = _mx_dequant(q, sc)
+    xf = x.double()
+    blk_max = xf.abs().view(rows, cols // 64, 64).amax(-1)
+    e = sc[:, :rows, :].permute(1, 0, 2).reshape(rows, cols // 64).double() - 127.0
+    # the scale is the smallest power of two keeping the block max <= 448
+    nz = blk_max > 0
+    assert (blk_max[nz] * torch.pow(2.0, -e[nz]) <= 448).all()
+    assert (blk_max[nz] * torch.pow(2.0, -e[nz]) > 224).all()
+    step = torch.pow(2.0, e).repeat_interleave(64, dim=1)
+    assert ((deq - xf).abs() <= 2.0 ** -4 * xf.abs() + step * 2.0 ** -9).all()
+
+
+@pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768 + 256, 1024), (300, 256, 128)])
+def test_gemm_fp8mx(dev, M, N, K):
+    torch.manual_seed(M + N * 3 + K)
+    a = torch.randn(M, K, device=dev) * torch.logspace(-2, 2, K // 64, device=dev).repeat_interleave(64)
+    w = torch.randn(N, K, device=dev) * K ** -0.5
+    a8 = torch.empty(M, K, device=dev, dtype=FP8)
+    asc = ops.mx_scales(M, K, dev, ld=M + 5)
+    ops.quant_fp8_mx(a, a8, asc)
+    w8, sw = _wq(w)
+    bias = torch.randn(N, device=dev) * 0.1
+    out = torch.empty(M, N, device=dev)
+    ops.gemm_fp8mx(a8, asc, w8, sw, out, bias=bias)
+    A = _mx_dequant(a8, asc)
+    Wd = w8.double() * sw.double()[:, None]
+    ref = A @ Wd.T + bias.double()
+    scale = A.abs() @ Wd.abs().T
+    err = (out.double() - ref).abs()
+    assert (err <= 3e-5 * scale + 1e-6).all(), (err / scale).max().item()
+
+
+def test_gemm_fp8mx_gelu_fp8_output_chain(dev):
+    """c_fc -> c_proj hand-off in fp8: the GELU epilogue writes e4m3 + its own e8m0 block
+    scales, which feed the next MX GEMM directly (no quantisation pass)."""
+    torch.manual_seed(11)
+    M, D, F = 577 * 4, 1024, 4096
+    h = torch.randn(M, D, device=dev)
+    wfc, wpr = torch.randn(F, D, device=dev) * D ** -0.5, torch.randn(D, F, device=dev) * F ** -0.5
+    bfc = torch.randn(F, device=dev) * 0.1
+    h8 = torch.empty(M, D, device=dev, dtype=FP8)
+    hsc = ops.mx_scales(M, D, dev)
+    ops.quant_fp8_mx(h, h8, hsc)
+    wfc8, sfc = _wq(wfc)
+    wpr8, spr = _wq(wpr)
+    f8 = torch.empty(M, F, device=dev, dtype=FP8)
+    fsc = ops.mx_scales(M, F, dev)
+    ops.gemm_fp8mx(h8, hsc, wfc8, sfc, f8, out_sc=fsc, bias=bfc, gelu=True)
+    # the fp8 GELU output vs GELU of the exact product of the quantised operands
+    g_ref = torch.nn.functional.gelu(_mx_dequant(h8, hsc) @ (wfc8.double() * sfc.double()[:, None]).T + bfc.double())
+    g = _mx_dequant(f8, fsc)
+    blk = g_ref.abs().view(M, F // 64, 64).amax(-1).repeat_interleave(64, dim=1)
+    assert ((g - g_ref).abs() <= 2.0 ** -4 * g_ref.abs() + blk * 2.0 ** -8 + 1e-4).all()
+    y = torch.empty(M, D, device=dev)
+    ops.gemm_fp8mx(f8, fsc, wpr8, spr, y)
+    y_ref = g @ (wpr8.double() * spr.double()[:, None]).T
+    scale = g.abs() @ (wpr8.double().abs() * spr.double()[:, None]).T
+    assert ((y.double() - y_ref).abs() <= 3e-5 * scale + 1e-6).all()
