@@ -10,7 +10,7 @@ import ctypes
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaaclip_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 F32 = 0
 BF16 = 1
@@ -38,9 +38,9 @@ SIGNATURES = {
     "aaclip_set_gemm_variant": [_I],
     "aaclip_attention": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "aaclip_im2col": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
-    "aaclip_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
-    "aaclip_block_tail": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
-    "aaclip_layernorm": [_I, _P, _L, _P, _P, _P, _L, _I, _I, _P],
+    "aaclip_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],
+    "aaclip_block_tail": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],
+    "aaclip_layernorm": [_I, _P, _L, _P, _P, _P, _L, _I, _I, _P, _L, _P],
     "aaclip_text_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "aaclip_eot_ln": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "aaclip_anchor_reduce": [_P, _I, _I, _P, _I, _I, _P],

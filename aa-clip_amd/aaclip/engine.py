@@ -172,32 +172,45 @@ class VisualEngine:
         X, H = ws["x"], ws["h"]
         ops.im2col(x, ws["cols"], PATCH)
         ops.gemm(ws["cols"], self.conv, X, row_group=P, row_group_out=n_tok, row_offset=1)
-        ops.embed_ln(X, self.cls, self.pos, self.ln_pre, self.blocks[0]["ln1"], H, B, n_tok)
         lvl = {lv: j for j, lv in enumerate(self.levels)}
         last = self.levels[-1]
         if self.fp8:
+            # every GEMM input is MX e4m3: the LayerNorm kernels and the c_fc epilogue
+            # write it directly; only the attention output goes through a quantisation pass
             a8, asc, f8, fsc = ws["a8"], ws["asc"], ws["f8"], ws["fsc"]
+            Hq, Hsc = a8, asc
+            ops.embed_ln(X, self.cls, self.pos, self.ln_pre, self.blocks[0]["ln1"], a8, B, n_tok, h_sc=asc)
 
-            def lin(a, w, out, **kw):  # MX e4m3 of the 1024-wide input, then the MX fp8 GEMM
-                ops.quant_fp8_mx(a, a8, asc)
-                ops.gemm_fp8mx(a8, asc, w[0], w[1], out, **kw)
+            def qkv(blk):
+                ops.gemm_fp8mx(a8, asc, blk["w_qkv"][0], blk["w_qkv"][1], ws["qkv"], bias=blk["b_qkv"])
+
+            def out_proj(blk):
+                ops.quant_fp8_mx(ws["attn"], a8, asc)
+                ops.gemm_fp8mx(a8, asc, blk["w_o"][0], blk["w_o"][1], X, bias=blk["b_o"], residual=X)
 
             def mlp(blk, aux):  # c_fc writes e4m3 + block scales that c_proj consumes directly
-                ops.quant_fp8_mx(H, a8, asc)
+                ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], a8, y_sc=asc)
                 ops.gemm_fp8mx(a8, asc, blk["w_fc"][0], blk["w_fc"][1], f8, out_sc=fsc, bias=blk["b_fc"], gelu=True)
                 ops.gemm_fp8mx(f8, fsc, blk["w_pr"][0], blk["w_pr"][1], X, bias=blk["b_pr"], residual=X, aux=aux)
         else:
-            lin = ops.gemm
+            Hq, Hsc = H, None
+            ops.embed_ln(X, self.cls, self.pos, self.ln_pre, self.blocks[0]["ln1"], H, B, n_tok)
+
+            def qkv(blk):
+                ops.gemm(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
+
+            def out_proj(blk):
+                ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
 
             def mlp(blk, aux):
+                ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], H)
                 ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True)
                 ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=aux)
         for i in range(last):
             blk = self.blocks[i]
-            lin(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
+            qkv(blk)
             ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS)
-            lin(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
-            ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], H)
+            out_proj(blk)
             adapt = i < self.adapt_until
             mlp(blk, ws["xb"] if (adapt and ws["xb"] is not None) else None)
             tap = ws["taps"][lvl[i + 1]] if (i + 1) in lvl else None
@@ -207,8 +220,8 @@ class VisualEngine:
                 ops.gemm(ws["xb"] if ws["xb"] is not None else X, self.w_adapt[i], ws["u"], leaky=True)
                 u = ws["u"]
             if u is not None or nxt is not None or tap is not None:
-                ops.block_tail(X, n_tok, u=u, adapt_weight=self.i_w, ln=nxt, h=H if nxt else None,
-                               post=self.ln_post, tap=tap)
+                ops.block_tail(X, n_tok, u=u, adapt_weight=self.i_w, ln=nxt, h=Hq if nxt else None,
+                               post=self.ln_post, tap=tap, h_sc=Hsc)
         L = len(self.levels)
         sb = ws["segbuf"]
         for j in range(L):

@@ -213,16 +213,27 @@ def im2col(img: torch.Tensor, cols: torch.Tensor, patch: int) -> torch.Tensor:
     return cols
 
 
-def embed_ln(x, cls, pos, ln_pre, ln1, h, batch, n_tok):
+def _mx_out(t, sc, rows):
+    """(dtype tag, scale ptr, ld) for an LN output: fp8 MX (t e4m3 + sc e8m0) or plain."""
+    if t is not None and t.dtype == FP8:
+        if sc is None or sc.dtype != torch.uint8 or sc.dim() != 3 or sc.shape[1] < rows or not t.is_contiguous():
+            raise ValueError("fp8 LayerNorm output needs a contiguous e4m3 tensor and MX scales [w/128, ld, 2]")
+        return _lib.FP8, _ptr(sc), sc.shape[1]
+    return (dtag(t) if t is not None else None), None, 0
+
+
+def embed_ln(x, cls, pos, ln_pre, ln1, h, batch, n_tok, h_sc=None):
     _dev(x, h)
     width = x.shape[1]
     if x.shape[0] != batch * n_tok or h.shape != x.shape or pos.shape != (n_tok, width):
         raise ValueError("embed_ln shape mismatch")
-    call("aaclip_embed_ln", dtag(h), _ptr(x), _ptr(cls), _ptr(pos), _ptr(ln_pre[0]), _ptr(ln_pre[1]),
-         _ptr(ln1[0]), _ptr(ln1[1]), _ptr(h), batch, n_tok, width, _stream())
+    od, scp, ld = _mx_out(h, h_sc, x.shape[0])
+    call("aaclip_embed_ln", od, _ptr(x), _ptr(cls), _ptr(pos), _ptr(ln_pre[0]), _ptr(ln_pre[1]),
+         _ptr(ln1[0]), _ptr(ln1[1]), _ptr(h), batch, n_tok, width, scp, ld, _stream())
 
 
-def block_tail(x, n_tok, *, u=None, adapt_weight=0.0, ln=None, h=None, post=None, tap=None, out_dtype=None):
+def block_tail(x, n_tok, *, u=None, adapt_weight=0.0, ln=None, h=None, post=None, tap=None, out_dtype=None,
+               h_sc=None):
     _dev(x, u, h, tap)
     rows, width = x.shape
     if u is not None and u.shape != x.shape:
@@ -231,23 +242,26 @@ def block_tail(x, n_tok, *, u=None, adapt_weight=0.0, ln=None, h=None, post=None
         raise ValueError("h shape mismatch")
     if tap is not None and tap.shape != (rows // n_tok * (n_tok - 1), width):
         raise ValueError("tap shape mismatch")
-    od = dtag(h) if h is not None else (dtag(tap) if tap is not None else F32)
-    if h is not None and tap is not None and h.dtype != tap.dtype:
-        raise ValueError("h and tap must share a dtype")
+    od, scp, ld = _mx_out(h, h_sc, rows)
+    if od is None:
+        od = dtag(tap) if tap is not None else F32
+    if h is not None and tap is not None and h.dtype != tap.dtype and not (h.dtype == FP8 and tap.dtype == torch.bfloat16):
+        raise ValueError("h and tap must share a dtype (or h fp8 MX with bf16 taps)")
     call("aaclip_block_tail", od, _ptr(x), _ptr(u), float(adapt_weight),
          _ptr(ln[0]) if ln else None, _ptr(ln[1]) if ln else None, _ptr(h),
          _ptr(post[0]) if post else None, _ptr(post[1]) if post else None, _ptr(tap),
-         rows, n_tok, width, _stream())
+         rows, n_tok, width, scp, ld, _stream())
 
 
-def layernorm(x, w, b, y):
+def layernorm(x, w, b, y, y_sc=None):
     _dev(x, y)
     _rowmajor(x, "x")
     _rowmajor(y, "y")
     if x.shape != y.shape or x.dtype != torch.float32:
         raise ValueError("layernorm shape/dtype mismatch")
-    call("aaclip_layernorm", dtag(y), _ptr(x), x.stride(0), _ptr(w), _ptr(b), _ptr(y), y.stride(0),
-         x.shape[0], x.shape[1], _stream())
+    od, scp, ld = _mx_out(y, y_sc, x.shape[0])
+    call("aaclip_layernorm", od, _ptr(x), x.stride(0), _ptr(w), _ptr(b), _ptr(y), y.stride(0),
+         x.shape[0], x.shape[1], scp, ld, _stream())
     return y
 
 

@@ -89,7 +89,50 @@ __device__ __forceinline__ void layer_norm(const float4_t (&x)[VEC], const float
   }
 }
 
-__device__ __forceinline__ size_t esize(int dtype) { return dtype == AACLIP_F32 ? 4 : 2; }
+__device__ __forceinline__ size_t esize(int dtype) { return dtype == AACLIP_F32 ? 4 : (dtype == AACLIP_BF16 ? 2 : 1); }
+
+// smallest e with amax * 2^-e <= 448 (largest finite e4m3): the e8m0 block scale
+__device__ __forceinline__ int mx_exp_row(float amax) {
+  if (!(amax > 0.f)) return 0;
+  int x;
+  (void)frexpf(amax, &x);  // amax = m * 2^x, m in [0.5, 1)
+  int e = x - 9;           // amax * 2^-e in [256, 512)
+  if (ldexpf(amax, -e) > 448.f) e += 1;
+  return max(min(e, 127), -126);
+}
+
+// MX fp8 row store (AACLIP_FP8 outputs, config C5): lane l holds elements 256c + 4l..+3,
+// so a 64-element block is 16 lanes: max over them (4 xor-shuffles inside the 16-lane
+// group), e8m0 scale, RNE to e4m3 after the exact 2^-e scaling; 4 bytes per lane and
+// chunk; the block's first lane writes the scale byte to sc[(blk/2)*ld_sc + row][blk%2].
+template <int VEC>
+__device__ __forceinline__ void store_mx(uint8_t* q, uint8_t* sc, int64_t ld_sc, size_t row,
+                                         const float4_t (&v)[VEC], int lane) {
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) {
+    float amax = fmaxf(fmaxf(fabsf(v[c][0]), fabsf(v[c][1])), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    const int e = mx_exp_row(amax);
+    const float inv = __uint_as_float((uint32_t)(127 - e) << 23);
+    uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][0] * inv, v[c][1] * inv, 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][2] * inv, v[c][3] * inv, w, true);
+    *(uint32_t*)(q + row * (256 * VEC) + 256 * c + 4 * lane) = w;
+    if ((lane & 15) == 0) {
+      const int blk = 4 * c + (lane >> 4);
+      sc[((size_t)(blk >> 1) * ld_sc + row) * 2 + (blk & 1)] = (uint8_t)(e + 127);
+    }
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_out(void* p, int dtype, size_t row, uint8_t* sc, int64_t ld_sc,
+                                          const float4_t (&v)[VEC], int lane) {
+  if (dtype == AACLIP_FP8)
+    store_mx<VEC>((uint8_t*)p, sc, ld_sc, row, v, lane);
+  else
+    store_any<VEC>((char*)p + row * (256 * VEC) * esize(dtype), dtype, v, lane);
+}
 
 // ------------------------------------------------------------------ kernels
 template <int VEC>
@@ -97,7 +140,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(int out_dtype, float* x, 
                                                        const float* pos, const float* pw,
                                                        const float* pb, const float* w1,
                                                        const float* b1, void* h, int rows,
-                                                       int n_tok) {
+                                                       int n_tok, uint8_t* sc, int64_t ld_sc) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -113,7 +156,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(int out_dtype, float* x, 
   layer_norm<VEC>(e, pw, pb, y, lane);
   store_any<VEC>(xr, AACLIP_F32, y, lane);
   layer_norm<VEC>(y, w1, b1, e, lane);
-  store_any<VEC>((char*)h + (size_t)row * D * esize(out_dtype), out_dtype, e, lane);
+  store_out<VEC>(h, out_dtype, row, sc, ld_sc, e, lane);
 }
 
 template <int VEC>
@@ -121,7 +164,8 @@ __global__ __launch_bounds__(256) void block_tail_kernel(int out_dtype, float* x
                                                          float aw, const float* lw,
                                                          const float* lb, void* h,
                                                          const float* pw, const float* pb,
-                                                         void* tap, int rows, int n_tok) {
+                                                         void* tap, int rows, int n_tok, uint8_t* sc,
+                                                         int64_t ld_sc) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -145,14 +189,15 @@ __global__ __launch_bounds__(256) void block_tail_kernel(int out_dtype, float* x
   float4_t y[VEC];
   if (h) {
     layer_norm<VEC>(v, lw, lb, y, lane);
-    store_any<VEC>((char*)h + (size_t)row * D * esize(out_dtype), out_dtype, y, lane);
+    store_out<VEC>(h, out_dtype, row, sc, ld_sc, y, lane);
   }
-  if (tap) {
+  if (tap) {  // level taps stay bf16/fp32 (seg_proj inputs) when h is fp8
+    const int tdt = out_dtype == AACLIP_FP8 ? AACLIP_BF16 : out_dtype;
     const int t = row % n_tok;
     if (t >= 1) {
       const size_t trow = (size_t)(row / n_tok) * (n_tok - 1) + (t - 1);
       layer_norm<VEC>(v, pw, pb, y, lane);
-      store_any<VEC>((char*)tap + trow * D * esize(out_dtype), out_dtype, y, lane);
+      store_any<VEC>((char*)tap + trow * D * esize(tdt), tdt, y, lane);
     }
   }
 }
@@ -160,14 +205,17 @@ __global__ __launch_bounds__(256) void block_tail_kernel(int out_dtype, float* x
 template <int VEC>
 __global__ __launch_bounds__(256) void layernorm_kernel(int out_dtype, const float* x, int64_t ldx,
                                                         const float* w, const float* b, void* y,
-                                                        int64_t ldy, int rows) {
+                                                        int64_t ldy, int rows, uint8_t* sc, int64_t ld_sc) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   float4_t v[VEC], o[VEC];
   load_f32<VEC>(x + (size_t)row * ldx, v, lane);
   layer_norm<VEC>(v, w, b, o, lane);
-  store_any<VEC>((char*)y + (size_t)row * ldy * esize(out_dtype), out_dtype, o, lane);
+  if (out_dtype == AACLIP_FP8)
+    store_mx<VEC>((uint8_t*)y, sc, ld_sc, row, o, lane);  // ldy == width (checked on the host)
+  else
+    store_any<VEC>((char*)y + (size_t)row * ldy * esize(out_dtype), out_dtype, o, lane);
 }
 
 template <int VEC>
@@ -315,6 +363,10 @@ __global__ __launch_bounds__(256) void im2col_kernel(int out_dtype, const float*
   }
 
 inline bool dtype_ok(int d) { return d == AACLIP_F32 || d == AACLIP_BF16; }
+// fp8 MX outputs (config C5) need the e8m0 scale buffer [width/128][ld_mx >= rows][2]
+inline bool mx_ok(int d, const void* mx, int64_t ld_mx, int rows, int width) {
+  return dtype_ok(d) || (d == AACLIP_FP8 && mx && ld_mx >= rows && width % 128 == 0);
+}
 
 
 // ------------------------------------------------------------------ fp8 quantisation
@@ -374,14 +426,6 @@ __global__ __launch_bounds__(256) void quant_fp8_kernel(int in_dtype, const void
 // MX variant: one wave per row, lane l owns elements 8l + 512c .. +7, so a 64-element
 // block is 8 consecutive lanes: max over them (3 xor-shuffles), power-of-two e8m0
 // scale, RNE to e4m3 after an exact 2^-e scaling.
-__device__ __forceinline__ int mx_exp_row(float amax) {
-  if (!(amax > 0.f)) return 0;
-  int x;
-  (void)frexpf(amax, &x);
-  int e = x - 9;
-  if (ldexpf(amax, -e) > 448.f) e += 1;
-  return max(min(e, 127), -126);
-}
 
 __global__ __launch_bounds__(256) void quant_mx_kernel(int in_dtype, const void* __restrict__ x, int64_t ldx,
                                                        uint8_t* __restrict__ q, int64_t ldq,
@@ -416,12 +460,14 @@ __global__ __launch_bounds__(256) void quant_mx_kernel(int in_dtype, const void*
 extern "C" int aaclip_embed_ln(int out_dtype, float* x, const float* cls, const float* pos,
                                const float* ln_pre_w, const float* ln_pre_b, const float* ln1_w,
                                const float* ln1_b, void* h, int batch, int n_tok, int width,
-                               void* stream) {
-  AACLIP_REQUIRE(dtype_ok(out_dtype) && x && cls && pos && ln_pre_w && ln_pre_b && ln1_w && ln1_b && h);
+                               void* h_mx, int64_t ld_mx, void* stream) {
+  AACLIP_REQUIRE(mx_ok(out_dtype, h_mx, ld_mx, batch * n_tok, width));
+  AACLIP_REQUIRE(x && cls && pos && ln_pre_w && ln_pre_b && ln1_w && ln1_b && h);
   AACLIP_REQUIRE(batch > 0 && n_tok > 1);
   const int rows = batch * n_tok;
   DISPATCH_VEC(width, embed_ln_kernel<V><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
-                          out_dtype, x, cls, pos, ln_pre_w, ln_pre_b, ln1_w, ln1_b, h, rows, n_tok));
+                          out_dtype, x, cls, pos, ln_pre_w, ln_pre_b, ln1_w, ln1_b, h, rows, n_tok,
+                          (uint8_t*)h_mx, ld_mx));
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -429,25 +475,27 @@ extern "C" int aaclip_embed_ln(int out_dtype, float* x, const float* cls, const 
 extern "C" int aaclip_block_tail(int out_dtype, float* x, const float* u, float adapt_weight,
                                  const float* ln_w, const float* ln_b, void* h,
                                  const float* post_w, const float* post_b, void* tap, int rows,
-                                 int n_tok, int width, void* stream) {
-  AACLIP_REQUIRE(dtype_ok(out_dtype) && x && rows > 0 && n_tok > 0);
+                                 int n_tok, int width, void* h_mx, int64_t ld_mx, void* stream) {
+  AACLIP_REQUIRE(mx_ok(out_dtype, h ? h_mx : (void*)1, h ? ld_mx : rows, rows, width));
+  AACLIP_REQUIRE(x && rows > 0 && n_tok > 0);
   AACLIP_REQUIRE(!h || (ln_w && ln_b));
   AACLIP_REQUIRE(!tap || (post_w && post_b && n_tok > 1 && rows % n_tok == 0));
   DISPATCH_VEC(width, block_tail_kernel<V><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
                           out_dtype, x, u, adapt_weight, ln_w, ln_b, h, post_w, post_b, tap, rows,
-                          n_tok));
+                          n_tok, (uint8_t*)h_mx, ld_mx));
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
 
 extern "C" int aaclip_layernorm(int out_dtype, const float* x, int64_t ldx, const float* w,
                                 const float* b, void* y, int64_t ldy, int rows, int width,
-                                void* stream) {
-  AACLIP_REQUIRE(dtype_ok(out_dtype) && x && w && b && y && rows >= 0);
+                                void* y_mx, int64_t ld_mx, void* stream) {
+  AACLIP_REQUIRE(mx_ok(out_dtype, y_mx, ld_mx, rows, width) && x && w && b && y && rows >= 0);
   AACLIP_REQUIRE(ldx >= width && ldy >= width && ldx % 4 == 0 && ldy % 4 == 0);
+  AACLIP_REQUIRE(out_dtype != AACLIP_FP8 || ldy == width);
   if (rows == 0) return AACLIP_OK;
   DISPATCH_VEC(width, layernorm_kernel<V><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
-                          out_dtype, x, ldx, w, b, y, ldy, rows));
+                          out_dtype, x, ldx, w, b, y, ldy, rows, (uint8_t*)y_mx, ld_mx));
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

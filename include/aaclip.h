@@ -42,7 +42,7 @@ extern "C" {
 #define AACLIP_EPI_RESID 8     /* + residual[row, n] (fp32; may alias C)    */
 #define AACLIP_EPI_AUX_BF16 16 /* also store a bf16 copy of the result      */
 
-/* ABI version (bumped on any signature change) and the compiled target. */
+/* ABI version (bumped on any signature change; 2 = MX fp8 LayerNorm outputs) and the target. */
 int aaclip_abi_version(void);
 const char* aaclip_arch(void);
 
@@ -159,7 +159,8 @@ int aaclip_im2col(int out_dtype, const float* img, void* cols, int batch, int ch
  */
 int aaclip_embed_ln(int out_dtype, float* x, const float* cls, const float* pos,
                     const float* ln_pre_w, const float* ln_pre_b, const float* ln1_w,
-                    const float* ln1_b, void* h, int batch, int n_tok, int width, void* stream);
+                    const float* ln1_b, void* h, int batch, int n_tok, int width,
+                    void* h_mx, int64_t ld_mx, void* stream);
 
 /*
  * Row epilogue after a residual block (all optional stages, one pass):
@@ -173,11 +174,20 @@ int aaclip_embed_ln(int out_dtype, float* x, const float* cls, const float* pos,
 int aaclip_block_tail(int out_dtype, float* x, const float* u, float adapt_weight,
                       const float* ln_w, const float* ln_b, void* h, const float* post_w,
                       const float* post_b, void* tap, int rows, int n_tok, int width,
-                      void* stream);
+                      void* h_mx, int64_t ld_mx, void* stream);
 
 /* y = LN(x) rows (F.layer_norm, eps 1e-5, biased variance; transformer.py:37-43). */
 int aaclip_layernorm(int out_dtype, const float* x, int64_t ldx, const float* w,
-                     const float* b, void* y, int64_t ldy, int rows, int width, void* stream);
+                     const float* b, void* y, int64_t ldy, int rows, int width,
+                     void* y_mx, int64_t ld_mx, void* stream);
+
+/*
+ * (embed_ln, block_tail, layernorm) out_dtype AACLIP_FP8: the LayerNorm row (h / y)
+ * is written as MX fp8 — e4m3 bytes [rows, width] plus an e8m0 scale per (row, 64
+ * columns) in h_mx / y_mx [width/128][ld_mx >= rows][2], the A-operand format of
+ * aaclip_gemm_fp8mx (config C5); level taps stay bf16. h_mx / ld_mx are ignored for
+ * the other dtypes (pass NULL, 0).
+ */
 
 /*
  * Text embedding: x[s*ctx+t] = tok_emb[tokens[s,t]] + pos[t]; h = LN_1(x).

@@ -36,7 +36,13 @@ def test_argument_validation_rejects_without_launch():
     assert lib.aaclip_gemm(5, 0, 8, 128, 64, None, 64, None, 64, None, 128, 0, None, None, 0, None, 0, 0, 0, 0, None) == 1
     assert lib.aaclip_attention(1, None, None, 1, 8, 1, 64, 0, None) == 1
     assert lib.aaclip_attention(1, ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 8, 1, 128, 0, None) == 1  # head_dim
-    assert lib.aaclip_layernorm(0, None, 512, None, None, None, 512, 4, 512, None) == 1
+    assert lib.aaclip_layernorm(0, None, 512, None, None, None, 512, 4, 512, None, 0, None) == 1
+    # fp8 MX outputs need their scale buffer; MX GEMM needs its operand scales
+    f16 = ctypes.c_void_p(16)
+    assert lib.aaclip_layernorm(2, f16, 1024, f16, f16, f16, 1024, 4, 1024, None, 0, None) == 1
+    assert lib.aaclip_gemm_fp8mx(0, 8, 256, 128, f16, 128, None, 8, f16, 128, f16, f16, 256, 0, None, None, 0,
+                                 None, 0, None, 0, None) == 1
+    assert lib.aaclip_quant_fp8_mx(1, f16, 100, f16, 128, f16, 4, 4, 100, None) == 1  # cols % 128
     assert lib.aaclip_blur_upsample(None, None, 1, 3, 24, 336, 7, 1.0, 0, None) == 1
     lv = (ctypes.c_void_p * 1)(16)
     assert lib.aaclip_patch_scores(1, lv, 1, 768, ctypes.c_void_p(16), 4, 512, 1, 0, 0, ctypes.c_void_p(16), None) == 1

@@ -206,3 +206,35 @@ def test_gemm_fp8mx_gelu_fp8_output_chain(dev):
     y_ref = g @ (wpr8.double() * spr.double()[:, None]).T
     scale = g.abs() @ (wpr8.double().abs() * spr.double()[:, None]).T
     assert ((y.double() - y_ref).abs() <= 3e-5 * scale + 1e-6).all()
+
+
+def test_layernorm_kernels_mx_output(dev):
+    """LayerNorm / block-tail / embed rows written straight to MX fp8 equal the MX
+    quantisation of the same kernels' fp32 rows, bit for bit (same fp32 values, same
+    scaling and rounding); block-tail taps stay bf16."""
+    torch.manual_seed(5)
+    R, W, n_tok = 577 * 3, 1024, 577
+    x = torch.randn(R, W, device=dev) * 3
+    w, b = torch.randn(W, device=dev), torch.randn(W, device=dev)
+    y32 = torch.empty(R, W, device=dev)
+    ops.layernorm(x, w, b, y32)
+    q_ref = torch.empty(R, W, device=dev, dtype=FP8)
+    s_ref = ops.mx_scales(R, W, dev)
+    ops.quant_fp8_mx(y32, q_ref, s_ref)
+    q = torch.empty(R, W, device=dev, dtype=FP8)
+    s = ops.mx_scales(R, W, dev)
+    ops.layernorm(x, w, b, q, y_sc=s)
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8)) and torch.equal(s, s_ref)
+    # block tail: adapter blend + next ln_1 (MX) + bf16 tap
+    u = torch.randn(R, W, device=dev)
+    post = (torch.randn(W, device=dev), torch.randn(W, device=dev))
+    x1, x2 = x.clone(), x.clone()
+    tap1 = torch.empty(R // n_tok * (n_tok - 1), W, device=dev, dtype=torch.bfloat16)
+    tap2 = torch.empty_like(tap1)
+    h32 = torch.empty(R, W, device=dev)
+    ops.block_tail(x1, n_tok, u=u, adapt_weight=0.1, ln=(w, b), h=h32, post=post, tap=None)
+    ops.block_tail(x2, n_tok, u=u, adapt_weight=0.1, ln=(w, b), h=q, post=post, tap=tap2, h_sc=s)
+    ops.quant_fp8_mx(h32, q_ref, s_ref)
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8)) and torch.equal(s, s_ref)
+    ops.block_tail(x.clone(), n_tok, u=u, adapt_weight=0.1, ln=None, h=None, post=post, tap=tap1)
+    assert torch.equal(tap1, tap2)
