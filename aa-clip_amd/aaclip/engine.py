@@ -175,8 +175,8 @@ class VisualEngine:
         lvl = {lv: j for j, lv in enumerate(self.levels)}
         last = self.levels[-1]
         if self.fp8:
-            # every GEMM input is MX e4m3: the LayerNorm kernels and the c_fc epilogue
-            # write it directly; only the attention output goes through a quantisation pass
+            # every GEMM input is MX e4m3, written directly by its producer: the LayerNorm
+            # kernels, the attention epilogue and the c_fc epilogue (no quantisation pass)
             a8, asc, f8, fsc = ws["a8"], ws["asc"], ws["f8"], ws["fsc"]
             Hq, Hsc = a8, asc
             ops.embed_ln(X, self.cls, self.pos, self.ln_pre, self.blocks[0]["ln1"], a8, B, n_tok, h_sc=asc)
@@ -184,8 +184,10 @@ class VisualEngine:
             def qkv(blk):
                 ops.gemm_fp8mx(a8, asc, blk["w_qkv"][0], blk["w_qkv"][1], ws["qkv"], bias=blk["b_qkv"])
 
+            def attend():  # attention epilogue writes the out-proj input as MX e4m3
+                ops.attention(ws["qkv"], a8, B, n_tok, HEADS, out_sc=asc)
+
             def out_proj(blk):
-                ops.quant_fp8_mx(ws["attn"], a8, asc)
                 ops.gemm_fp8mx(a8, asc, blk["w_o"][0], blk["w_o"][1], X, bias=blk["b_o"], residual=X)
 
             def mlp(blk, aux):  # c_fc writes e4m3 + block scales that c_proj consumes directly
@@ -199,6 +201,9 @@ class VisualEngine:
             def qkv(blk):
                 ops.gemm(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
 
+            def attend():
+                ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS)
+
             def out_proj(blk):
                 ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
 
@@ -209,7 +214,7 @@ class VisualEngine:
         for i in range(last):
             blk = self.blocks[i]
             qkv(blk)
-            ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS)
+            attend()
             out_proj(blk)
             adapt = i < self.adapt_until
             mlp(blk, ws["xb"] if (adapt and ws["xb"] is not None) else None)

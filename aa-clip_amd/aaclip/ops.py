@@ -189,14 +189,25 @@ def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux):
 
 # ------------------------------------------------------------------------ attention
 def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int,
-              causal: bool = False) -> torch.Tensor:
-    _dev(qkv, out)
+              causal: bool = False, out_sc=None) -> torch.Tensor:
+    """out = MHA core of packed qkv; out fp8 (e4m3) + out_sc = MX output (bf16 qkv only)."""
+    _dev(qkv, out, out_sc)
     hd = 64
     if qkv.shape != (batch * seq, 3 * heads * hd) or out.shape != (batch * seq, heads * hd):
         raise ValueError("attention shape mismatch")
-    if not (qkv.is_contiguous() and out.is_contiguous()) or qkv.dtype != out.dtype:
-        raise ValueError("attention tensors must be contiguous and share a dtype")
-    call("aaclip_attention", dtag(qkv), _ptr(qkv), _ptr(out), batch, seq, heads, hd, int(causal), _stream())
+    if not (qkv.is_contiguous() and out.is_contiguous()):
+        raise ValueError("attention tensors must be contiguous")
+    if out.dtype == FP8:
+        if qkv.dtype != torch.bfloat16 or out_sc is None or out_sc.dtype != torch.uint8 or \
+                out_sc.shape[0] != heads // 2 or out_sc.shape[1] < batch * seq:
+            raise ValueError("fp8 attention output needs bf16 qkv and MX scales [heads/2, ld, 2]")
+        call("aaclip_attention", _lib.FP8, _ptr(qkv), _ptr(out), batch, seq, heads, hd, int(causal),
+             _ptr(out_sc), out_sc.shape[1], _stream())
+        return out
+    if qkv.dtype != out.dtype:
+        raise ValueError("attention tensors must share a dtype")
+    call("aaclip_attention", dtag(qkv), _ptr(qkv), _ptr(out), batch, seq, heads, hd, int(causal), None, 0,
+         _stream())
     return out
 
 

@@ -164,7 +164,8 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
 
 __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
                                                         uint16_t* __restrict__ out, int N, int H,
-                                                        int causal) {
+                                                        int causal, uint8_t* __restrict__ out_mx,
+                                                        int64_t ld_mx) {
   constexpr int NS = ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) char smem[NS * 2 * KT * 128];  // [stage][K|V][64][128B]
   const int lane = threadIdx.x & 63;
@@ -280,6 +281,56 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
 #undef ATTN_WAIT_BARRIER
 
   // ---- epilogue: O[q][d = db*16 + 4g + i] = ot / l
+  if (out_mx) {
+    // MX fp8 output (config C5, the out-proj input): one head = one 64-column block,
+    // held by the 4 lanes {c, c+16, c+32, c+48}: block max over them, e8m0 scale,
+    // RNE e4m3, 4x4 dword transpose so lane g owns columns 16g..16g+15 -> 16-B stores
+    uint8_t* o8 = (uint8_t*)out;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const float inv = 1.0f / l_acc[qb][0];
+      const int q = q0 + qb * 16 + c;
+      float amax = 0.f;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(ot[qb][db][i] * inv));
+      amax = max_over_groups(amax);
+      int e = 0;
+      if (amax > 0.f) {
+        int x;
+        (void)frexpf(amax, &x);
+        e = x - 9;
+        if (ldexpf(amax, -e) > 448.f) e += 1;
+        e = max(min(e, 127), -126);
+      }
+      const float s = inv * __uint_as_float((uint32_t)(127 - e) << 23);
+      uint32_t d[4];
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(ot[qb][db][0] * s, ot[qb][db][1] * s, 0, false);
+        d[db] = __builtin_amdgcn_cvt_pk_fp8_f32(ot[qb][db][2] * s, ot[qb][db][3] * s, w, true);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        auto r = __builtin_amdgcn_permlane32_swap(d[j], d[j + 2], false, false);
+        d[j] = r[0];
+        d[j + 2] = r[1];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k += 2) {
+        auto r = __builtin_amdgcn_permlane16_swap(d[k], d[k + 1], false, false);
+        d[k] = r[0];
+        d[k + 1] = r[1];
+      }
+      if (q < N) {
+        const size_t row = (size_t)b * N + q;
+        *(uint4*)(o8 + row * HDt + h * HD_ + 16 * g) = uint4{d[0], d[1], d[2], d[3]};
+        if (g == 0) out_mx[((size_t)(h >> 1) * ld_mx + row) * 2 + (h & 1)] = (uint8_t)(e + 127);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const float inv = 1.0f / l_acc[qb][0];
@@ -367,14 +418,17 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(const float* __restrict__ 
 }  // namespace
 
 extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
-                                int heads, int head_dim, int causal, void* stream) {
-  AACLIP_REQUIRE(dtype == AACLIP_F32 || dtype == AACLIP_BF16);
+                                int heads, int head_dim, int causal, void* out_mx, int64_t ld_mx,
+                                void* stream) {
+  AACLIP_REQUIRE(dtype == AACLIP_F32 || dtype == AACLIP_BF16 || dtype == AACLIP_FP8);
   AACLIP_REQUIRE(qkv && out && batch > 0 && seq > 0 && heads > 0 && head_dim == HD_);
+  AACLIP_REQUIRE(dtype != AACLIP_FP8 || (out_mx && ld_mx >= (int64_t)batch * seq && heads % 2 == 0));
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == AACLIP_BF16) {
+  if (dtype != AACLIP_F32) {  // bf16 compute; fp8 = bf16 inputs with an MX e4m3 output
     const long nwg = (long)ceil_div(seq, QT) * batch * heads;
     AACLIP_REQUIRE(nwg < (1L << 31));
-    attn_bf16_kernel<<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, seq, heads, causal);
+    attn_bf16_kernel<<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, seq, heads, causal,
+                                                   dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr, ld_mx);
   } else {
     dim3 grid(ceil_div(seq, 64), batch * heads);
     attn_f32_kernel<<<grid, 64, 0, s>>>((const float*)qkv, (float*)out, seq, heads, causal);

@@ -140,7 +140,11 @@ int aaclip_set_gemm_variant(int variant);
  * discarded by the caller, model/adapter.py:91 — never computed here).
  */
 int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
-                     int heads, int head_dim, int causal, void* stream);
+                     int heads, int head_dim, int causal, void* out_mx, int64_t ld_mx,
+                     void* stream);
+/* dtype AACLIP_FP8: bf16 qkv in, out written as MX e4m3 [batch*seq, heads*64] with one
+ * e8m0 scale per (row, head) in out_mx [heads/2][ld_mx >= batch*seq][2] (the out-proj
+ * A operand of aaclip_gemm_fp8mx, config C5); out_mx ignored otherwise. */
 
 /*
  * Patchify for conv1-as-GEMM: img [batch, channels, S, S] fp32 ->

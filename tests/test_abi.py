@@ -34,8 +34,9 @@ def test_argument_validation_rejects_without_launch():
     lib = _lib.lib()
     # null operands / bad dtype / unsupported shapes return AACLIP_ERR_ARG (=1)
     assert lib.aaclip_gemm(5, 0, 8, 128, 64, None, 64, None, 64, None, 128, 0, None, None, 0, None, 0, 0, 0, 0, None) == 1
-    assert lib.aaclip_attention(1, None, None, 1, 8, 1, 64, 0, None) == 1
-    assert lib.aaclip_attention(1, ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 8, 1, 128, 0, None) == 1  # head_dim
+    assert lib.aaclip_attention(1, None, None, 1, 8, 1, 64, 0, None, 0, None) == 1
+    assert lib.aaclip_attention(1, ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 8, 1, 128, 0, None, 0, None) == 1
+    assert lib.aaclip_attention(2, ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 8, 2, 64, 0, None, 0, None) == 1
     assert lib.aaclip_layernorm(0, None, 512, None, None, None, 512, 4, 512, None, 0, None) == 1
     # fp8 MX outputs need their scale buffer; MX GEMM needs its operand scales
     f16 = ctypes.c_void_p(16)

@@ -238,3 +238,45 @@ def test_layernorm_kernels_mx_output(dev):
     assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8)) and torch.equal(s, s_ref)
     ops.block_tail(x.clone(), n_tok, u=u, adapt_weight=0.1, ln=None, h=None, post=post, tap=tap1)
     assert torch.equal(tap1, tap2)
+
+
+@pytest.mark.parametrize("B,N", [(2, 577), (1, 1025), (3, 130)])
+def test_attention_mx_output(dev, B, N):
+    """The attention epilogue's MX e4m3 output (one e8m0 scale per (row, head)) equals the MX
+    quantisation of its fp32-accurate output up to one e4m3 code, and dequantises to the
+    bf16 kernel's output within e4m3 precision."""
+    torch.manual_seed(B * N)
+    H = 16
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev).bfloat16()
+    o_bf = torch.empty(B * N, H * 64, device=dev, dtype=torch.bfloat16)
+    ops.attention(qkv, o_bf, B, N, H)
+    o8 = torch.empty(B * N, H * 64, device=dev, dtype=FP8)
+    sc = ops.mx_scales(B * N, H * 64, dev)
+    ops.attention(qkv, o8, B, N, H, out_sc=sc)
+    deq = _mx_dequant(o8, sc)
+    ref = o_bf.double()
+    blk = ref.abs().view(B * N, H, 64).amax(-1).repeat_interleave(64, dim=1)
+    assert ((deq - ref).abs() <= 2.0 ** -4 * ref.abs() + 2.0 ** -8 * blk + 1e-3).all()
+
+
+def test_attention_mx_output_not_worse_than_requantised_bf16(dev):
+    """Quantising in the attention epilogue (from fp32) must be at least as accurate as
+    quantising the bf16 output afterwards (double rounding): mean |error| vs the fp32
+    attention kernel, and codes differ from the requantised bf16 ones by at most one."""
+    torch.manual_seed(3)
+    B, N, H = 2, 577, 16
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev).bfloat16()
+    o32 = torch.empty(B * N, H * 64, device=dev)
+    ops.attention(qkv.float(), o32, B, N, H)
+    o_bf = torch.empty(B * N, H * 64, device=dev, dtype=torch.bfloat16)
+    ops.attention(qkv, o_bf, B, N, H)
+    o8 = torch.empty(B * N, H * 64, device=dev, dtype=FP8)
+    sc = ops.mx_scales(B * N, H * 64, dev)
+    ops.attention(qkv, o8, B, N, H, out_sc=sc)
+    r8 = torch.empty_like(o8)
+    rsc = ops.mx_scales(B * N, H * 64, dev)
+    ops.quant_fp8_mx(o_bf, r8, rsc)
+    e_new = (_mx_dequant(o8, sc) - o32.double()).abs().mean().item()
+    e_old = (_mx_dequant(r8, rsc) - o32.double()).abs().mean().item()
+    assert e_new <= e_old * 1.01, (e_new, e_old)
+    assert torch.equal(sc, rsc) or (sc.int() - rsc.int()).abs().max().item() <= 1
