@@ -8,7 +8,8 @@ parameters; the packed device copies are rebuilt whenever a parameter changes
 (load_state_dict, in-place edits: tracked by tensor version counters).
 
 Compute dtype of the visual tower: bf16 MFMA by default (`compute_dtype=
-torch.float32` selects the fp32-MFMA parity mode; env AACLIP_DTYPE=fp32 too).
+torch.float32` selects the fp32-MFMA parity mode, `torch.float8_e4m3fn` the config-C5
+fp8 MX mode; env AACLIP_DTYPE=fp32 / fp8 too).
 The text tower always runs fp32 (once per dataset, <1% of the work).
 """
 from __future__ import annotations
@@ -28,6 +29,8 @@ def param_signature(module: nn.Module, prefix_excl: str | None = None):
 
 def _default_dtype():
     v = os.environ.get("AACLIP_DTYPE", "bf16").lower()
+    if v in ("fp8", "float8", "e4m3"):  # config C5: fp8 MX block GEMMs
+        return torch.float8_e4m3fn
     return torch.float32 if v in ("fp32", "float32", "f32") else torch.bfloat16
 
 

@@ -68,7 +68,7 @@ def main(argv=None):
     parser.add_argument("--allow_random_init", action="store_true",
                         help="run on random-init CLIP + adapters when no checkpoints exist")
     parser.add_argument("--synthetic_n", type=int, default=16)
-    parser.add_argument("--compute_dtype", type=str, default="bf16", choices=["bf16", "fp32"])
+    parser.add_argument("--compute_dtype", type=str, default="bf16", choices=["bf16", "fp32", "fp8"])
     args = parser.parse_args(argv)
 
     setup_seed(args.seed)
@@ -88,7 +88,8 @@ def main(argv=None):
     model = AdaptedCLIP(clip_model=clip_model, text_adapt_weight=args.text_adapt_weight,
                         image_adapt_weight=args.image_adapt_weight, text_adapt_until=args.text_adapt_until,
                         image_adapt_until=args.image_adapt_until, relu=args.relu,
-                        compute_dtype=torch.float32 if args.compute_dtype == "fp32" else torch.bfloat16).to(device)
+                        compute_dtype={"fp32": torch.float32, "fp8": torch.float8_e4m3fn}.get(
+                            args.compute_dtype, torch.bfloat16)).to(device)
     model.eval()
 
     text_file = glob(args.save_path + "/text_adapter.pth")
