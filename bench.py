@@ -199,7 +199,7 @@ def c5_leg(dev, steps: int, warmup: int, streams: int, batch: int = 32):
             t_qa = time_launches(lambda: ops.quant_fp8_mx(ws["h"], a8, asc), 10, st)
             fl = 2.0 * R * WIDTH * 7 * WIDTH / 2
             ach = fl / ((t_q + t_f) / 2 * 1e-3) / 1e12
-            out["fp8_gemm_roofline"] = {"kernel": "gemm_bf16_kernel<256,256,2,4,MX> (QKV + c_fc launches)",
+            out["fp8_gemm_roofline"] = {"kernel": "gemm_fp8mx_8ph_kernel (QKV + c_fc launches)",
                                         "bound": "mfma", "unit": "TFLOP/s", "achieved": round(ach, 1),
                                         "peak": 2 * BF16_PEAK_TFLOPS, "frac": round(ach / (2 * BF16_PEAK_TFLOPS), 4),
                                         "avg_launch_us": round((t_q + t_f) / 2 * 1e3, 2),

@@ -7,10 +7,19 @@ error against the fp32 reference path is reported by tests/test_e2e_gpu.py."""
 import pytest
 import torch
 
-from aaclip import ops
+from aaclip import _lib, ops
 
 pytestmark = pytest.mark.gpu
 FP8 = torch.float8_e4m3fn
+
+
+@pytest.fixture(params=[0, 6], ids=["mx8ph", "mx256"])
+def mx_variant(request):
+    """MX GEMM kernel family: 0 = the default 8-phase ping-pong kernel with the
+    3-slot scale ring, 6 = the 256x256 LDS-DMA kernel."""
+    _lib.call("aaclip_set_gemm_variant", request.param)
+    yield request.param
+    _lib.call("aaclip_set_gemm_variant", 0)
 
 
 def _quant_ref(x):
@@ -161,7 +170,7 @@ def test_quant_fp8_mx(dev, dtype, rows, cols):
 
 
 @pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768 + 256, 1024), (300, 256, 128)])
-def test_gemm_fp8mx(dev, M, N, K):
+def test_gemm_fp8mx(dev, mx_variant, M, N, K):
     torch.manual_seed(M + N * 3 + K)
     a = torch.randn(M, K, device=dev) * torch.logspace(-2, 2, K // 64, device=dev).repeat_interleave(64)
     w = torch.randn(N, K, device=dev) * K ** -0.5
@@ -180,7 +189,7 @@ def test_gemm_fp8mx(dev, M, N, K):
     assert (err <= 3e-5 * scale + 1e-6).all(), (err / scale).max().item()
 
 
-def test_gemm_fp8mx_gelu_fp8_output_chain(dev):
+def test_gemm_fp8mx_gelu_fp8_output_chain(dev, mx_variant):
     """c_fc -> c_proj hand-off in fp8: the GELU epilogue writes e4m3 + its own e8m0 block
     scales, which feed the next MX GEMM directly (no quantisation pass)."""
     torch.manual_seed(11)
@@ -206,6 +215,31 @@ def test_gemm_fp8mx_gelu_fp8_output_chain(dev):
     y_ref = g @ (wpr8.double() * spr.double()[:, None]).T
     scale = g.abs() @ (wpr8.double().abs() * spr.double()[:, None]).T
     assert ((y.double() - y_ref).abs() <= 3e-5 * scale + 1e-6).all()
+
+
+def test_gemm_fp8mx_8ph_race_screen(dev):
+    """The 8-phase MX kernel places its LDS hand-offs (tiles and the scale ring) by
+    vmcnt/barrier counting; repeated launches must be bit-identical."""
+    torch.manual_seed(5)
+    M, N, K = 577 * 8, 4096, 1024
+    a = torch.randn(M, K, device=dev) * torch.logspace(-1, 1, K // 64, device=dev).repeat_interleave(64)
+    a8 = torch.empty(M, K, device=dev, dtype=FP8)
+    asc = ops.mx_scales(M, K, dev)
+    ops.quant_fp8_mx(a, a8, asc)
+    w8, sw = _wq(torch.randn(N, K, device=dev) * K ** -0.5)
+    outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+    try:
+        ops.gemm_fp8mx(a8, asc, w8, sw, outs[0])
+        _lib.call("aaclip_set_gemm_variant", 6)
+        ref = torch.empty_like(outs[0])
+        ops.gemm_fp8mx(a8, asc, w8, sw, ref)
+        assert torch.equal(outs[0], ref)  # same fp32 sums in the same K order
+        _lib.call("aaclip_set_gemm_variant", 0)
+        for _ in range(12):
+            ops.gemm_fp8mx(a8, asc, w8, sw, outs[1])
+            assert torch.equal(outs[0], outs[1])
+    finally:
+        _lib.call("aaclip_set_gemm_variant", 0)
 
 
 def test_layernorm_kernels_mx_output(dev):

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--shapes", default="qkv,out,fc,proj,adapter", help="GEMM shapes to run")
     ap.add_argument("--map", action="store_true", help="also run the anomaly-map stream kernel (C2 sizes)")
     ap.add_argument("--fp8", action="store_true", help="also time the fp8 GEMM (+ the row quantisation of A)")
+    ap.add_argument("--mx", action="store_true", help="also time the fp8 MX GEMM per --variants (0 vs 5)")
     ap.add_argument("--tokens", type=int, default=577, help="tokens per image (577 @336 px, 1025 @448 px)")
     ap.add_argument("--torch", action="store_true",
                     help="also time torch (hipBLASLt) on the same GEMM shapes, for comparison only")
@@ -92,6 +93,34 @@ def main():
                 res[f"{name}/fp8"] = (ms, 2.0 * R * N * K / ms / 1e9)
                 ms = timeit(lambda: ops.quant_fp8_rows(a, a8, sa), args.reps)
                 res[f"{name}/quantA"] = (ms, R * K * 3 / ms / 1e9)
+        if args.mx:
+            FP8 = torch.float8_e4m3fn
+            mx = {}
+            for name, (N, K, kw, a, w, bias, out) in data.items():
+                a8 = torch.empty(R, K, device=dev, dtype=FP8)
+                asc = ops.mx_scales(R, K, dev)
+                ops.quant_fp8_mx(a.float(), a8, asc)
+                sw = (w.float().abs().amax(1) / 448).contiguous()
+                w8 = (w.float() / sw[:, None]).to(FP8)
+                if kw.get("gelu"):  # c_fc writes fp8 MX for c_proj
+                    o8, osc = torch.empty(R, N, device=dev, dtype=FP8), ops.mx_scales(R, N, dev)
+                else:
+                    o8, osc = out, None
+                mx[name] = (N, K, kw, a8, asc, w8, sw, bias, o8, osc)
+            for rnd_i in range(args.rounds):
+                for v in variants:
+                    _lib.call("aaclip_set_gemm_variant", v)
+                    for name, (N, K, kw, a8, asc, w8, sw, bias, o8, osc) in mx.items():
+                        f = lambda: ops.gemm_fp8mx(a8, asc, w8, sw, o8, out_sc=osc,  # noqa: E731
+                                                   bias=bias if kw.get("bias") else None, gelu=kw.get("gelu", False),
+                                                   leaky=kw.get("leaky", False),
+                                                   residual=o8 if kw.get("resid") else None)
+                        ms = timeit(f, args.reps)
+                        key = f"{name}/mx/v{v}"
+                        prev = res.get(key)
+                        if prev is None or ms < prev[0]:
+                            res[key] = (ms, 2.0 * R * N * K / ms / 1e9)
+            _lib.call("aaclip_set_gemm_variant", 0)
         if args.torch:  # library comparison: linear (+bias) -> epilogue in torch ops
             F = torch.nn.functional
             for name, (N, K, kw, a, w, bias, out) in data.items():
