@@ -1,0 +1,351 @@
+// Test-time preprocessing on device: the reference's
+// transform_x = Resize((S,S), BICUBIC) -> ToTensor -> Normalize(CLIP) and
+// transform_mask = Resize((S,S), NEAREST) -> ToTensor -> != 0
+// (dataset/__init__.py:127-143, applied at :152-162). torchvision hands PIL
+// images to Pillow, so the arithmetic restated here is Pillow's, bit for bit:
+//
+//   * plan (host, double precision, same expression order as Pillow's
+//     precompute_coeffs / normalize_coeffs_8bpc): per output coordinate the
+//     first source tap and the tap count, and int32 weights with 22 fraction
+//     bits (a = -0.5 cubic, support 2 * max(in/out, 1), normalised to sum 1);
+//   * kernel: two 8-bit passes, horizontal first. One workgroup owns a tile of
+//     TY output rows x 64 output columns of one image: it resamples the source
+//     rows that tile's vertical taps touch into an LDS strip of uint8 (each
+//     value clipped exactly like Pillow's intermediate image), then runs the
+//     vertical taps out of LDS and writes float32 (v / 255 - mean) / std
+//     (IEEE division, as torch's div_) into the CHW plane layout the visual
+//     embed reads. Source bytes are read once per tap through L1/L2; the
+//     strip is the only LDS traffic.
+//   * masks: nearest index tables (Pillow's accumulated xo += in/out) and a
+//     one-pass gather writing (v != 0) as float32.
+//
+// HBM bytes per image: H*W*3 read + 3*S*S*4 written (+ the tiny plans).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+constexpr int PREC = 22;  // Pillow PRECISION_BITS for 8-bit images
+constexpr int NT = 256;   // threads per workgroup
+
+__device__ __forceinline__ uint32_t clip8(int v) {
+  v >>= PREC;  // arithmetic shift, as Pillow's lookup index
+  return (uint32_t)min(max(v, 0), 255);
+}
+
+struct PrepArgs {
+  const uint8_t* src;
+  int64_t img_stride, pitch;
+  int in_h, in_w, S, ty, tx;
+  const int32_t *xb, *xk, *yb, *yk;
+  int kx, ky;
+  float mean[3], stdv[3];
+  float* out;
+  int tiles_x, tiles_y, max_rows, max_cols, srow;
+};
+
+// One workgroup = ty output rows x tx output columns of one image.
+// STAGED: the source patch the tile touches (rows r0..r1, columns c0..c1) is
+// first copied into LDS with aligned dword loads (every load of the tile in
+// flight at once, coalesced along the row), so the tap loops below read LDS
+// instead of waiting on one scattered byte load per tap. Direct: taps read the
+// source through L1/L2 (only for extreme downscales whose patch exceeds LDS).
+template <bool STAGED>
+__global__ __launch_bounds__(NT) void bicubic_normalize_kernel(PrepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  // STAGED layout: tap weights of the tile's columns [tx][kx] and rows [ty][ky] (int32),
+  // then the horizontal-pass strip [max_rows][tx][3], then the source patch [max_rows][srow]
+  int32_t* kxs = (int32_t*)lds;
+  int32_t* kys = kxs + (STAGED ? a.tx * a.kx : 0);
+  uint8_t* strip = (uint8_t*)(kys + (STAGED ? a.ty * a.ky : 0));
+  uint8_t* patch = strip + ((a.max_rows * a.tx * 3 + 15) & ~15);
+  const int tile = blockIdx.x;
+  const int b = blockIdx.y;
+  const int txi = tile % a.tiles_x, tyi = tile / a.tiles_x;
+  const int x0 = txi * a.tx, y0 = tyi * a.ty;
+  const int y1 = min(y0 + a.ty, a.S), x1 = min(x0 + a.tx, a.S);
+  const int r0 = a.yb[2 * y0];
+  // r1 - r0 <= (ty-1)*in/S + 2*support + 1 <= max_rows (strip_bound); the min only guards LDS
+  const int nrows = min(a.yb[2 * (y1 - 1)] + a.yb[2 * (y1 - 1) + 1] - r0, a.max_rows);
+  const uint8_t* img = a.src + (size_t)b * a.img_stride;
+  const int c0 = a.xb[2 * x0];
+
+  if constexpr (STAGED) {
+    const int ncols = min(a.xb[2 * (x1 - 1)] + a.xb[2 * (x1 - 1) + 1] - c0, a.max_cols);
+    const int ndw = (ncols * 3 + 3 + 3) >> 2;  // dwords per row incl. the <= 3-byte alignment shift
+    // 8 independent loads in flight per thread before the first LDS write (a
+    // one-load-per-iteration loop serialises on HBM latency: measured 4x slower)
+    constexpr int U = 8;
+    const int total = nrows * ndw;
+    for (int i0 = threadIdx.x; i0 < total; i0 += NT * U) {
+      uint32_t v[U];
+      int dst[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * NT;
+        dst[u] = -1;
+        if (i < total) {
+          const int r = i / ndw, d = i - r * ndw;
+          const uintptr_t row = (uintptr_t)(img + (size_t)(r0 + r) * a.pitch + (size_t)c0 * 3);
+          const uintptr_t base = row & ~(uintptr_t)3;  // aligned dwords never cross a page: no fault past the end
+          if ((int)(row - base) + ncols * 3 > d * 4) {
+            v[u] = *(const uint32_t*)(base + 4 * (uintptr_t)d);
+            dst[u] = r * a.srow + 4 * d;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (dst[u] >= 0) *(uint32_t*)(patch + dst[u]) = v[u];
+    }
+    for (int i = threadIdx.x; i < (x1 - x0) * a.kx; i += NT) kxs[i] = a.xk[(size_t)x0 * a.kx + i];
+    for (int i = threadIdx.x; i < (y1 - y0) * a.ky; i += NT) kys[i] = a.yk[(size_t)y0 * a.ky + i];
+    __syncthreads();
+  }
+
+  // pass 1: horizontal taps for source rows r0..r1 of this tile's columns
+  for (int i = threadIdx.x; i < nrows * a.tx; i += NT) {
+    const int r = i / a.tx, xo = i - r * a.tx, x = x0 + xo;
+    if (x >= x1) continue;
+    const int xmin = a.xb[2 * x], n = a.xb[2 * x + 1];
+    const int32_t* k = STAGED ? kxs + xo * a.kx : a.xk + (size_t)x * a.kx;
+    const uint8_t* p;
+    if constexpr (STAGED) {
+      const uintptr_t row = (uintptr_t)(img + (size_t)(r0 + r) * a.pitch + (size_t)c0 * 3);
+      p = patch + r * a.srow + (int)(row & 3) + (xmin - c0) * 3;
+    } else {
+      p = img + (size_t)(r0 + r) * a.pitch + (size_t)xmin * 3;
+    }
+    int s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
+#pragma unroll 4
+    for (int t = 0; t < n; ++t) {
+      const int w = k[t];
+      s0 += (int)p[3 * t + 0] * w;
+      s1 += (int)p[3 * t + 1] * w;
+      s2 += (int)p[3 * t + 2] * w;
+    }
+    uint8_t* d = strip + (r * a.tx + xo) * 3;
+    d[0] = (uint8_t)clip8(s0);
+    d[1] = (uint8_t)clip8(s1);
+    d[2] = (uint8_t)clip8(s2);
+  }
+  __syncthreads();
+
+  // pass 2: vertical taps out of LDS, normalise, CHW fp32 stores (consecutive x per wave)
+  const size_t plane = (size_t)a.S * a.S;
+  float* ob = a.out + (size_t)b * 3 * plane;
+  for (int i = threadIdx.x; i < (y1 - y0) * a.tx; i += NT) {
+    const int yo = i / a.tx, xo = i - yo * a.tx, x = x0 + xo, y = y0 + yo;
+    if (x >= x1) continue;
+    const int ymin = a.yb[2 * y] - r0, n = a.yb[2 * y + 1];
+    const int32_t* k = STAGED ? kys + yo * a.ky : a.yk + (size_t)y * a.ky;
+    int s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
+#pragma unroll 4
+    for (int t = 0; t < n; ++t) {
+      const int w = k[t];
+      const uint8_t* q = strip + ((ymin + t) * a.tx + xo) * 3;
+      s0 += (int)q[0] * w;
+      s1 += (int)q[1] * w;
+      s2 += (int)q[2] * w;
+    }
+    const size_t o = (size_t)y * a.S + x;
+    ob[o] = ((float)clip8(s0) / 255.0f - a.mean[0]) / a.stdv[0];
+    ob[plane + o] = ((float)clip8(s1) / 255.0f - a.mean[1]) / a.stdv[1];
+    ob[2 * plane + o] = ((float)clip8(s2) / 255.0f - a.mean[2]) / a.stdv[2];
+  }
+}
+
+__global__ __launch_bounds__(NT) void nearest_mask_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
+                                                          int64_t pitch, const int32_t* __restrict__ xi,
+                                                          const int32_t* __restrict__ yi, int S,
+                                                          float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const size_t plane = (size_t)S * S;
+  for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < plane; i += (size_t)gridDim.x * NT) {
+    const int y = (int)(i / S), x = (int)(i - (size_t)y * S);
+    const uint8_t v = src[(size_t)b * img_stride + (size_t)yi[y] * pitch + xi[x]];
+    out[(size_t)b * plane + i] = v != 0 ? 1.0f : 0.0f;
+  }
+}
+
+double bicubic_filter(double x) {
+  const double a = -0.5;
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+  if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+  return 0.0;
+}
+
+int bicubic_ksize(int in_size, int out_size) {
+  double filterscale = (double)in_size / out_size;
+  if (filterscale < 1.0) filterscale = 1.0;
+  return (int)ceil(2.0 * filterscale) * 2 + 1;
+}
+
+// source rows (or columns) the taps of `t` consecutive output coordinates can touch:
+// (t-1)*in/S + 2*support + 1 <= ceil((t-1)*in/S) + ksize + 2
+int strip_bound(int in_size, int S, int t, int ksize) {
+  const double scale = (double)in_size / S;
+  return min(in_size, (int)ceil((t - 1) * scale) + ksize + 2);
+}
+
+constexpr int STAGED_LDS = 64 * 1024;   // staged tiles: patch + strip
+constexpr int DIRECT_LDS = 128 * 1024;  // direct tiles: strip only
+
+}  // namespace
+
+extern "C" int aaclip_bicubic_taps(int in_size, int out_size, int* ksize) {
+  AACLIP_REQUIRE(in_size > 0 && out_size > 0 && ksize);
+  *ksize = bicubic_ksize(in_size, out_size);
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_bicubic_plan(int in_size, int out_size, int32_t* bounds, int32_t* coeffs, int ksize) {
+#pragma clang fp contract(off)
+  AACLIP_REQUIRE(in_size > 0 && out_size > 0);
+  const int need = bicubic_ksize(in_size, out_size);
+  AACLIP_REQUIRE(bounds && coeffs && ksize >= need);
+  const double scale = (double)in_size / out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 2.0 * filterscale;
+  std::vector<double> w(need);
+  for (int xx = 0; xx < out_size; ++xx) {
+    const double center = (xx + 0.5) * scale;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    double ww = 0.0;
+    for (int x = 0; x < xmax; ++x) {
+      w[x] = bicubic_filter((x + xmin - center + 0.5) * ss);
+      ww += w[x];
+    }
+    int32_t* k = coeffs + (size_t)xx * ksize;
+    for (int x = 0; x < ksize; ++x) {
+      if (x >= xmax) {
+        k[x] = 0;
+        continue;
+      }
+      const double v = ww != 0.0 ? w[x] / ww : w[x];
+      k[x] = v < 0 ? (int32_t)(-0.5 + v * (1 << PREC)) : (int32_t)(0.5 + v * (1 << PREC));
+    }
+    bounds[2 * xx] = xmin;
+    bounds[2 * xx + 1] = xmax;
+  }
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_nearest_plan(int in_size, int out_size, int32_t* index) {
+#pragma clang fp contract(off)
+  AACLIP_REQUIRE(in_size > 0 && out_size > 0 && index);
+  const double a = (double)in_size / out_size;
+  double xo = a * 0.5;
+  for (int x = 0; x < out_size; ++x) {
+    index[x] = xo < 0.0 ? -1 : (int32_t)xo;
+    xo += a;
+  }
+  for (int x = 0; x < out_size; ++x) AACLIP_REQUIRE(index[x] >= 0 && index[x] < in_size);
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_preprocess_images(const uint8_t* src, int64_t img_stride, int64_t row_pitch, int batch,
+                                        int in_h, int in_w, const int32_t* x_bounds, const int32_t* x_coeffs,
+                                        int kx, const int32_t* y_bounds, const int32_t* y_coeffs, int ky,
+                                        int out_size, const float* mean_std, float* out, void* stream) {
+  AACLIP_REQUIRE(src && x_bounds && x_coeffs && y_bounds && y_coeffs && out && batch >= 0);
+  AACLIP_REQUIRE(in_h > 0 && in_w > 0 && out_size > 0 && row_pitch >= (int64_t)in_w * 3);
+  AACLIP_REQUIRE(img_stride >= row_pitch * in_h || batch <= 1);
+  AACLIP_REQUIRE(kx >= bicubic_ksize(in_w, out_size) && ky >= bicubic_ksize(in_h, out_size));
+  if (batch == 0) return AACLIP_OK;
+  PrepArgs a{};
+  a.src = src;
+  a.img_stride = img_stride;
+  a.pitch = row_pitch;
+  a.in_h = in_h;
+  a.in_w = in_w;
+  a.S = out_size;
+  a.xb = x_bounds;
+  a.xk = x_coeffs;
+  a.yb = y_bounds;
+  a.yk = y_coeffs;
+  a.kx = kx;
+  a.ky = ky;
+  static const float clip_mean_std[6] = {0.48145466f, 0.4578275f, 0.40821073f,
+                                         0.26862954f, 0.26130258f, 0.27577711f};
+  const float* ms = mean_std ? mean_std : clip_mean_std;
+  for (int c = 0; c < 3; ++c) {
+    a.mean[c] = ms[c];
+    a.stdv[c] = ms[3 + c];
+  }
+  a.out = out;
+  // tile choice: the tallest/widest staged tile (from 16 x 32) whose weights + strip + patch
+  // fit STAGED_LDS, else direct taps. 1024 -> 336: 16 x 32 tiles, 62 x 111-pixel patches,
+  // 32 KB -> 4 workgroups per CU. Measured at B=32 1024^2 (tools/prep_sweep.sh):
+  // 16x64 257 us, 8x64 195, 16x32 152, 16x16 144, direct 257 -- occupancy-bound.
+  bool staged = false;
+  int lds = 0;
+  int ty_max = 16, tx_max = 32, force_direct = 0;
+  if (const char* e = getenv("AACLIP_PREP_TILE")) sscanf(e, "%d,%d,%d", &ty_max, &tx_max, &force_direct);  // tuning
+  for (int tx = tx_max; tx >= 16 && !staged && !force_direct; tx >>= 1)
+    for (int ty = ty_max; ty >= 1 && !staged; ty >>= 1) {
+      const int rows = strip_bound(in_h, out_size, ty, ky), cols = strip_bound(in_w, out_size, tx, kx);
+      const int srow = (cols * 3 + 3 + 3 + 15) & ~15;
+      const int bytes = (tx * kx + ty * ky) * 4 + ((rows * tx * 3 + 15) & ~15) + rows * srow;
+      if (bytes <= STAGED_LDS) {
+        staged = true;
+        a.ty = ty;
+        a.tx = tx;
+        a.max_rows = rows;
+        a.max_cols = cols;
+        a.srow = srow;
+        lds = bytes;
+      }
+    }
+  if (!staged) {
+    a.tx = 64;
+    a.ty = 16;
+    while (a.ty > 1 && strip_bound(in_h, out_size, a.ty, ky) * a.tx * 3 > DIRECT_LDS) a.ty >>= 1;
+    a.max_rows = strip_bound(in_h, out_size, a.ty, ky);
+    lds = a.max_rows * a.tx * 3;
+    AACLIP_REQUIRE(lds <= DIRECT_LDS);
+  }
+  a.tiles_x = ceil_div(out_size, a.tx);
+  a.tiles_y = ceil_div(out_size, a.ty);
+  AACLIP_REQUIRE(batch <= 65535 && (int64_t)a.tiles_x * a.tiles_y < (1ll << 31));
+  static bool attr_set = false;  // benign race: idempotent attribute writes
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)bicubic_normalize_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            STAGED_LDS) != hipSuccess ||
+        hipFuncSetAttribute((const void*)bicubic_normalize_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            DIRECT_LDS) != hipSuccess)
+      return AACLIP_ERR_LAUNCH;
+    attr_set = true;
+  }
+  const dim3 grid(a.tiles_x * a.tiles_y, batch);
+  if (staged)
+    bicubic_normalize_kernel<true><<<grid, NT, lds, (hipStream_t)stream>>>(a);
+  else
+    bicubic_normalize_kernel<false><<<grid, NT, lds, (hipStream_t)stream>>>(a);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_resize_masks_nearest(const uint8_t* src, int64_t img_stride, int64_t row_pitch, int batch,
+                                           int in_h, int in_w, const int32_t* x_index, const int32_t* y_index,
+                                           int out_size, float* out, void* stream) {
+  AACLIP_REQUIRE(src && x_index && y_index && out && batch >= 0 && in_h > 0 && in_w > 0 && out_size > 0);
+  AACLIP_REQUIRE(row_pitch >= in_w && (img_stride >= row_pitch * in_h || batch <= 1) && batch <= 65535);
+  if (batch == 0) return AACLIP_OK;
+  const size_t plane = (size_t)out_size * out_size;
+  const int blocks = (int)std::min<size_t>((plane + NT - 1) / NT, 1024);
+  nearest_mask_kernel<<<dim3(blocks, batch), NT, 0, (hipStream_t)stream>>>(src, img_stride, row_pitch, x_index,
+                                                                           y_index, out_size, out);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}

@@ -9,6 +9,11 @@ relative to the working directory, images under DATA_PATH[dataset].
 Extra: dataset name "synthetic" (no files needed) yields seeded N(0,1)
 post-normalisation images and rectangle masks.
 Training datasets/augmentation are out of scope.
+
+raw=True (build extension): items carry the decoded uint8
+image [H, W, 3] and mask [H, W] instead of the transformed tensors; batch them
+with `collate_raw` and transform on the GPU with aaclip.preprocess.Preprocessor,
+which is bit-exact with the Pillow transform above (tests/test_preprocess.py).
 """
 from __future__ import annotations
 
@@ -26,9 +31,10 @@ STD = np.array((0.26862954, 0.26130258, 0.27577711), np.float32)[:, None, None]
 
 
 class BaseSingleClassDataset(Dataset):
-    def __init__(self, data_path: str, meta_path: str, img_size: int, class_name: str, logger=None):
+    def __init__(self, data_path: str, meta_path: str, img_size: int, class_name: str, logger=None,
+                 raw: bool = False):
         assert class_name is not None, "class_name should be provided"
-        self.data_path, self.img_size = data_path, img_size
+        self.data_path, self.img_size, self.raw = data_path, img_size, raw
         self.meta = []
         with open(meta_path) as f:
             for line in f:
@@ -54,8 +60,20 @@ class BaseSingleClassDataset(Dataset):
         m = Image.open(path).convert("L").resize((self.img_size, self.img_size), Image.NEAREST)
         return torch.from_numpy((np.asarray(m) != 0).astype(np.float32))[None]
 
+    def _raw_item(self, meta):
+        from PIL import Image
+        img = np.asarray(Image.open(os.path.join(self.data_path, meta["image_path"])).convert("RGB"))
+        if meta["label"]:
+            m = np.asarray(Image.open(os.path.join(self.data_path, meta["mask_path"])).convert("L"))
+        else:
+            m = np.zeros(img.shape[:2], np.uint8)
+        return {"image_u8": torch.from_numpy(img.copy()), "mask_u8": torch.from_numpy(m.copy()),
+                "label": meta["label"], "file_name": meta["image_path"], "class_name": meta["class_name"]}
+
     def __getitem__(self, idx):
         meta = self.meta[idx]
+        if self.raw:
+            return self._raw_item(meta)
         img = self._image(os.path.join(self.data_path, meta["image_path"]))
         if meta["label"]:
             mask = self._mask(os.path.join(self.data_path, meta["mask_path"]))
@@ -90,8 +108,18 @@ class SyntheticSingleClassDataset(Dataset):
                 "file_name": f"synthetic/{idx:05d}.png", "class_name": self.class_name}
 
 
+def collate_raw(items):
+    """Batch raw items: uint8 images/masks stacked when the sizes agree (one
+    preprocessing launch), else kept as lists (one launch per size)."""
+    out = {k: [it[k] for it in items] for k in items[0]}
+    for k in ("image_u8", "mask_u8"):
+        if len({tuple(t.shape) for t in out[k]}) == 1:
+            out[k] = torch.stack(out[k])
+    return out
+
+
 def get_dataset(dataset_name: str, img_size: int, training_mode: str, shot: int = -1, stage: str = "train",
-                logger=None, synthetic_n: int = 16):
+                logger=None, synthetic_n: int = 16, raw: bool = False):
     if dataset_name == "synthetic":
         if stage not in ("test", "visualize"):
             raise ValueError("the synthetic dataset only has a test stage")
@@ -104,6 +132,6 @@ def get_dataset(dataset_name: str, img_size: int, training_mode: str, shot: int 
     if stage in ("test", "visualize"):
         meta_path = os.path.join("./dataset/metadata", dataset_name, "full-shot.jsonl")
         return {c: BaseSingleClassDataset(DATA_PATH[dataset_name], meta_path, img_size, c,
-                                          logger=logger if stage == "test" else None)
+                                          logger=logger if stage == "test" else None, raw=raw)
                 for c in CLASS_NAMES[dataset_name]}
     raise ValueError(f"stage {stage} not found; available stages: train, test")

@@ -31,13 +31,26 @@ from model.clip import create_model  # noqa: E402
 from utils import setup_seed  # noqa: E402
 
 
-def get_predictions(model, class_text_embeddings, test_loader, device, img_size, dataset="MVTec"):
+def _device_batch(input_data, prep, device):
+    """Raw uint8 batch (dataset raw=True) -> transformed image / mask tensors on the
+    GPU (aaclip_preprocess_images / aaclip_resize_masks_nearest)."""
+    def run(fn, u8):
+        if isinstance(u8, torch.Tensor):
+            return fn(u8.to(device, non_blocking=True))
+        return torch.cat([fn(t.to(device, non_blocking=True)[None]) for t in u8])
+    return run(prep.images, input_data["image_u8"]), run(prep.masks, input_data["mask_u8"])
+
+
+def get_predictions(model, class_text_embeddings, test_loader, device, img_size, dataset="MVTec", prep=None):
     masks, labels, preds, preds_image, file_names = [], [], [], [], []
     for input_data in test_loader:
-        image = input_data["image"].to(device, non_blocking=True)
+        if prep is not None:
+            image, mask = _device_batch(input_data, prep, device)
+        else:
+            image, mask = input_data["image"].to(device, non_blocking=True), input_data["mask"]
         class_name = input_data["class_name"]
         assert len(set(class_name)) == 1, "mixed class not supported"
-        masks.append(input_data["mask"].cpu().numpy())
+        masks.append(mask.cpu().numpy())
         labels.append(np.asarray(input_data["label"]))
         file_names.extend(input_data["file_name"])
         pmap, score = model.predict(image, class_text_embeddings, DOMAINS[dataset])
@@ -69,6 +82,8 @@ def main(argv=None):
                         help="run on random-init CLIP + adapters when no checkpoints exist")
     parser.add_argument("--synthetic_n", type=int, default=16)
     parser.add_argument("--compute_dtype", type=str, default="bf16", choices=["bf16", "fp32", "fp8"])
+    parser.add_argument("--gpu_preprocess", action="store_true",
+                        help="decode on the host, resize + normalise on the GPU (bit-exact with the Pillow path)")
     args = parser.parse_args(argv)
 
     setup_seed(args.seed)
@@ -115,19 +130,26 @@ def main(argv=None):
         logger.info("-----------------------------------------------")
         logger.info("load model from epoch %d", test_epoch)
         logger.info("-----------------------------------------------")
+        raw = args.gpu_preprocess and args.dataset != "synthetic"  # synthetic items are already normalised
         image_datasets = get_dataset(args.dataset, args.img_size, None, args.shot, "test", logger=logger,
-                                     synthetic_n=args.synthetic_n)
+                                     synthetic_n=args.synthetic_n, raw=raw)
+        prep = None
+        if raw:
+            from aaclip.preprocess import Preprocessor
+            prep = Preprocessor(args.img_size)
         with torch.no_grad():
             text_embeddings = get_adapted_text_embedding(model if adapt_text else clip_model, args.dataset, device)
         df = DataFrame(columns=["class name", "pixel AUC", "pixel AP", "image AUC", "image AP"])
         for class_name, image_dataset in image_datasets.items():
             workers = 0 if args.dataset == "synthetic" else 4
+            from dataset import collate_raw
             loader = torch.utils.data.DataLoader(image_dataset, batch_size=args.batch_size, shuffle=False,
-                                                 num_workers=workers, pin_memory=True)
+                                                 num_workers=workers, pin_memory=True,
+                                                 collate_fn=collate_raw if raw else None)
             with torch.no_grad():
                 masks, labels, preds, preds_image, file_names = get_predictions(
                     model=model, class_text_embeddings=text_embeddings[class_name], test_loader=loader,
-                    device=device, img_size=args.img_size, dataset=args.dataset)
+                    device=device, img_size=args.img_size, dataset=args.dataset, prep=prep)
             if args.visualize:
                 visualize(masks, preds.cpu().numpy(), file_names, args.save_path, args.dataset, class_name=class_name)
             result = metrics_eval(masks, labels, preds, preds_image, class_name, domain=DOMAINS[args.dataset])

@@ -284,6 +284,40 @@ int aaclip_metrics_eval(const float* pixel_preds, const uint8_t* pixel_label, co
                         const uint8_t* image_label, int n_images, int64_t pix_per_image, int medical,
                         void* workspace, size_t workspace_bytes, double* out, void* stream);
 
+/*
+ * Test-time preprocessing (replaces dataset/__init__.py:127-143
+ * transform_x / transform_mask, i.e. Pillow's Image.resize as torchvision calls it,
+ * then ToTensor + Normalize). Bit-exact with Pillow 8-bit resampling.
+ *
+ * Host-only plan builders (no device work): Pillow BICUBIC per-axis tables --
+ * bounds [out_size, 2] int32 = (first source tap, tap count), coeffs
+ * [out_size, ksize] int32 with 22 fraction bits; aaclip_bicubic_taps gives the
+ * ksize to allocate. Nearest: index [out_size] int32 (Pillow's accumulated
+ * in/out stepping).
+ */
+int aaclip_bicubic_taps(int in_size, int out_size, int* ksize);
+int aaclip_bicubic_plan(int in_size, int out_size, int32_t* bounds, int32_t* coeffs, int ksize);
+int aaclip_nearest_plan(int in_size, int out_size, int32_t* index);
+
+/*
+ * src: batch uint8 RGB images [in_h, in_w, 3] (row pitch / image stride in
+ * bytes); plans (device copies) from aaclip_bicubic_plan(in_w, S) and (in_h, S).
+ * out: fp32 [batch, 3, S, S] = (bicubic(src) / 255 - mean) / std; mean_std:
+ * host float[6] (mean rgb, std rgb) or NULL for the CLIP constants.
+ */
+int aaclip_preprocess_images(const uint8_t* src, int64_t img_stride, int64_t row_pitch, int batch,
+                             int in_h, int in_w, const int32_t* x_bounds, const int32_t* x_coeffs,
+                             int kx, const int32_t* y_bounds, const int32_t* y_coeffs, int ky,
+                             int out_size, const float* mean_std, float* out, void* stream);
+
+/*
+ * src: batch uint8 L masks [in_h, in_w]; out fp32 [batch, 1, S, S] =
+ * (nearest-resized mask != 0). Index tables from aaclip_nearest_plan (device copies).
+ */
+int aaclip_resize_masks_nearest(const uint8_t* src, int64_t img_stride, int64_t row_pitch, int batch,
+                                int in_h, int in_w, const int32_t* x_index, const int32_t* y_index,
+                                int out_size, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

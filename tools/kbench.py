@@ -151,12 +151,26 @@ def main():
         grid = torch.empty(P, device=dev)
         ms = timeit(lambda: ops.patch_scores(levels, T, grid), args.reps)
         res["patch_scores"] = (ms, (4 * P * 768 * 4 + P * 4) / ms / 1e6)
+    if args.only == "prep":  # device preprocessing: B decoded 1024x1024 RGB -> fp32 [B,3,S,S] (+ masks)
+        from aaclip.preprocess import Preprocessor
+        S = 336 if args.tokens == 577 else 448
+        for H in (900, 1024):
+            u8 = torch.randint(0, 256, (B, H, H, 3), device=dev, dtype=torch.uint8)
+            m8 = (torch.rand(B, H, H, device=dev) < 0.1).to(torch.uint8)
+            pp = Preprocessor(S)
+            out = torch.empty(B, 3, S, S, device=dev)
+            mo = torch.empty(B, 1, S, S, device=dev)
+            ms = timeit(lambda: pp.images(u8, out), args.reps)
+            res[f"prep{H}"] = (ms, (u8.numel() + out.numel() * 4) / ms / 1e6)
+            ms = timeit(lambda: pp.masks(m8, mo), args.reps)
+            res[f"mask{H}"] = (ms, (B * S * S * (1 + 4)) / ms / 1e6)
     if args.only in ("", "rows"):
         lw, lb = rnd(W), rnd(W)
         ms = timeit(lambda: ops.layernorm(x, lw, lb, h), args.reps)
         res["layernorm"] = (ms, (R * W * 6) / ms / 1e6)
     for k, (ms, rate) in res.items():
-        unit = "GB/s" if k in ("layernorm", "patch_scores") or k.endswith("quantA") else "TFLOP/s"
+        unit = "GB/s" if k in ("layernorm", "patch_scores") or k.endswith("quantA") or k[:4] in ("prep", "mask") \
+            else "TFLOP/s"
         print(f"{k:10s} {ms * 1e3:9.1f} us  {rate:8.1f} {unit}")
 
 
