@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaaclip_hip.so")
+LIB_PATH = os.environ.get("AACLIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaaclip_hip.so")
 ABI_VERSION = 2
 
 F32 = 0
@@ -20,6 +20,8 @@ EPI_GELU = 2
 EPI_LEAKY = 4
 EPI_RESID = 8
 EPI_AUX_BF16 = 16
+ATTN_CAUSAL = 1
+ATTN_Q_PRESCALED = 2
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

@@ -27,6 +27,7 @@ from . import ops
 
 WIDTH = 1024
 HEADS = 16
+Q_LOG2_SCALE = 0.125 * 1.4426950408889634  # 1/sqrt(64) * log2(e)
 LAYERS = 24
 PATCH = 14
 EMBED = 768
@@ -57,7 +58,7 @@ def _quant_weight_fp8(w: torch.Tensor):
 
 class VisualEngine:
     def __init__(self, vparams: dict, adapter: dict, *, levels=(6, 12, 18, 24), image_adapt_until=6,
-                 image_adapt_weight=0.1, dtype=torch.bfloat16):
+                 image_adapt_weight=0.1, dtype=torch.bfloat16, fold_q_scale=True):
         """dtype: bfloat16 (perf path), float32 (parity mode) or float8_e4m3fn (config C5:
         the four block GEMMs per layer run on e4m3 weights (per-output-channel scales) and
         MX e4m3 activations (e8m0 scale per 64 values, applied by the K=128 block-scaled
@@ -87,13 +88,25 @@ class VisualEngine:
         self.pos = f32(vparams["visual.positional_embedding"])
         self.ln_pre = (f32(vparams["visual.ln_pre.weight"]), f32(vparams["visual.ln_pre.bias"]))
         self.ln_post = (f32(vparams["visual.ln_post.weight"]), f32(vparams["visual.ln_post.bias"]))
+        # bf16/fp8: the attention softmax runs in the log2 domain on q' = q * log2(e)/8;
+        # the factor is folded into the Q rows of in_proj (weights and bias, in fp32
+        # before the bf16/e4m3 rounding), so no per-score scaling remains in the kernel
+        self.q_prescaled = dtype != torch.float32 and fold_q_scale  # False: the kernel scales Q at load (A/B)
+
+        def qkv_param(t):
+            t = t.detach().to(dev, torch.float32).clone()
+            if self.q_prescaled:
+                t[:WIDTH] *= Q_LOG2_SCALE
+            return t.contiguous()
+
         self.blocks = []
         for i in range(LAYERS):
             p = f"visual.transformer.resblocks.{i}."
             self.blocks.append(dict(
                 ln1=(f32(vparams[p + "ln_1.weight"]), f32(vparams[p + "ln_1.bias"])),
                 ln2=(f32(vparams[p + "ln_2.weight"]), f32(vparams[p + "ln_2.bias"])),
-                w_qkv=cdt(vparams[p + "attn.in_proj_weight"]), b_qkv=f32(vparams[p + "attn.in_proj_bias"]),
+                w_qkv=cdt(qkv_param(vparams[p + "attn.in_proj_weight"])),
+                b_qkv=qkv_param(vparams[p + "attn.in_proj_bias"]),
                 w_o=cdt(vparams[p + "attn.out_proj.weight"]), b_o=f32(vparams[p + "attn.out_proj.bias"]),
                 w_fc=cdt(vparams[p + "mlp.c_fc.weight"]), b_fc=f32(vparams[p + "mlp.c_fc.bias"]),
                 w_pr=cdt(vparams[p + "mlp.c_proj.weight"]), b_pr=f32(vparams[p + "mlp.c_proj.bias"]),
@@ -185,7 +198,7 @@ class VisualEngine:
                 ops.gemm_fp8mx(a8, asc, blk["w_qkv"][0], blk["w_qkv"][1], ws["qkv"], bias=blk["b_qkv"])
 
             def attend():  # attention epilogue writes the out-proj input as MX e4m3
-                ops.attention(ws["qkv"], a8, B, n_tok, HEADS, out_sc=asc)
+                ops.attention(ws["qkv"], a8, B, n_tok, HEADS, out_sc=asc, q_prescaled=self.q_prescaled)
 
             def out_proj(blk):
                 ops.gemm_fp8mx(a8, asc, blk["w_o"][0], blk["w_o"][1], X, bias=blk["b_o"], residual=X)
@@ -202,7 +215,7 @@ class VisualEngine:
                 ops.gemm(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
 
             def attend():
-                ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS)
+                ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS, q_prescaled=self.q_prescaled)
 
             def out_proj(blk):
                 ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)

@@ -189,9 +189,13 @@ def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux):
 
 # ------------------------------------------------------------------------ attention
 def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int,
-              causal: bool = False, out_sc=None) -> torch.Tensor:
-    """out = MHA core of packed qkv; out fp8 (e4m3) + out_sc = MX output (bf16 qkv only)."""
+              causal: bool = False, out_sc=None, q_prescaled: bool = False) -> torch.Tensor:
+    """out = MHA core of packed qkv; out fp8 (e4m3) + out_sc = MX output (bf16 qkv only).
+    q_prescaled: the q columns already carry log2(e)/sqrt(64) (bf16 qkv only)."""
     _dev(qkv, out, out_sc)
+    flags = (_lib.ATTN_CAUSAL if causal else 0) | (_lib.ATTN_Q_PRESCALED if q_prescaled else 0)
+    if q_prescaled and qkv.dtype != torch.bfloat16:
+        raise ValueError("q_prescaled needs bf16 qkv")
     hd = 64
     if qkv.shape != (batch * seq, 3 * heads * hd) or out.shape != (batch * seq, heads * hd):
         raise ValueError("attention shape mismatch")
@@ -201,12 +205,12 @@ def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads:
         if qkv.dtype != torch.bfloat16 or out_sc is None or out_sc.dtype != torch.uint8 or \
                 out_sc.shape[0] != heads // 2 or out_sc.shape[1] < batch * seq:
             raise ValueError("fp8 attention output needs bf16 qkv and MX scales [heads/2, ld, 2]")
-        call("aaclip_attention", _lib.FP8, _ptr(qkv), _ptr(out), batch, seq, heads, hd, int(causal),
+        call("aaclip_attention", _lib.FP8, _ptr(qkv), _ptr(out), batch, seq, heads, hd, flags,
              _ptr(out_sc), out_sc.shape[1], _stream())
         return out
     if qkv.dtype != out.dtype:
         raise ValueError("attention tensors must share a dtype")
-    call("aaclip_attention", dtag(qkv), _ptr(qkv), _ptr(out), batch, seq, heads, hd, int(causal), None, 0,
+    call("aaclip_attention", dtag(qkv), _ptr(qkv), _ptr(out), batch, seq, heads, hd, flags, None, 0,
          _stream())
     return out
 

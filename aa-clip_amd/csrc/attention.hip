@@ -47,25 +47,34 @@ __device__ __forceinline__ float max_over_groups(float v) {
 // 16-query blocks (1 or 2), MASK = tile needs the key-tail / causal mask.
 // Dead blocks and the mask are resolved at compile time, so the 577 = 9*64 + 1
 // key tail costs 1/4 of a tile and full tiles carry no masking code.
-// Scores stay unscaled until the exponent: max on raw S (the scale is > 0),
-// p = exp2(S * log2e/8 - m2) as one FMA + one v_exp_f32. The O rescale is
-// skipped when no row max in the wave moved (alpha == 1 everywhere).
+// Q arrives pre-scaled by log2(e)/sqrt(64) (folded into the Q projection by the
+// caller, or applied to the Q fragments at load), so S' = K.Q^T is already in
+// the log2 domain, and the QK^T accumulator is initialised to -m (m = this
+// query's running max): the MFMA delivers S' - m and p = exp2(S' - m) is one
+// v_exp_f32 per score, no FMA. The running max is DEFERRED: it only moves when
+// a tile's max exceeds it by more than 2^8 (kRescaleLog2), so p <= 256 and the
+// O/l rescale (and the shift of this tile's scores) runs on the first tile and
+// then almost never. The result is the same softmax: O and l carry the same
+// factor 2^-m.
 // The softmax denominator is one more MFMA per 32 keys: an all-ones A operand
 // against the same bf16 P^T fragment gives sum_k p[k][q] in every accumulator
 // row (lane-local, already reduced over keys), replacing 16 v_add per 16 queries
 // per tile on an issue-bound loop; numerator and denominator then use the same
 // bf16-rounded p.
+constexpr float kRescaleLog2 = 8.0f;
+
 template <int NKB, int NQB, bool MASK>
 __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&qf)[2][2], float4_t (&ot)[2][4],
                                           float (&m_run)[2], float4_t (&l_acc)[2], int key0, int q0, int N,
-                                          int causal, int g, int c) {
-  constexpr float sl2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+                                          int causal, int g, int c, bool first) {
   const char* vt_lds = kt_lds + KT * 128;
   float4_t st[NQB][NKB];
 #pragma unroll
-  for (int qb = 0; qb < NQB; ++qb)
+  for (int qb = 0; qb < NQB; ++qb) {
+    const float nm = -m_run[qb];
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) st[qb][kb] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < NKB; ++kb) st[qb][kb] = float4_t{nm, nm, nm, nm};
+  }
 #pragma unroll
   for (int kb = 0; kb < NKB; ++kb) {
 #pragma unroll
@@ -99,24 +108,27 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[qb][kb][i]);
     }
-    mx = max_over_groups(mx);
-    const float m_old = m_run[qb];
-    const float m_new = fmaxf(m_old, mx * sl2);
-    m_run[qb] = m_new;
-    float p[2 * NKS][4];
-#pragma unroll
-    for (int kb = 0; kb < 2 * NKS; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        p[kb][i] = kb < NKB ? __builtin_amdgcn_exp2f(fmaf(st[qb][kb < NKB ? kb : 0][i], sl2, -m_new)) : 0.f;
-    if (__builtin_amdgcn_ballot_w64(m_new != m_old) != 0) {  // wave-uniform
-      const float alpha = __builtin_amdgcn_exp2f(m_old - m_new);
+    mx = max_over_groups(mx);  // max over the tile of S' - m for this lane's query
+    const bool move = first || mx > kRescaleLog2;
+    if (__builtin_amdgcn_ballot_w64(move) != 0) {  // wave-uniform branch, rare after the first tile
+      const float d = move ? mx : 0.f;          // tile 0 always has a valid key: mx is finite
+      m_run[qb] += d;
+      const float alpha = __builtin_amdgcn_exp2f(-d);
       l_acc[qb][0] *= alpha;  // only element 0 is read at the end
 #pragma unroll
       for (int db = 0; db < 4; ++db)
 #pragma unroll
         for (int e = 0; e < 4; ++e) ot[qb][db][e] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st[qb][kb][i] -= d;
     }
+    float p[2 * NKS][4];
+#pragma unroll
+    for (int kb = 0; kb < 2 * NKS; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) p[kb][i] = kb < NKB ? __builtin_amdgcn_exp2f(st[qb][kb < NKB ? kb : 0][i]) : 0.f;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       bf16x8_t v;
@@ -163,9 +175,10 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
 #endif
 
 __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
-                                                        uint16_t* __restrict__ out, int N, int H,
-                                                        int causal, uint8_t* __restrict__ out_mx,
+                                                        uint16_t* __restrict__ out, int batch, int N, int H,
+                                                        int flags, uint8_t* __restrict__ out_mx,
                                                         int64_t ld_mx) {
+  const int causal = flags & AACLIP_ATTN_CAUSAL;
   constexpr int NS = ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) char smem[NS * 2 * KT * 128];  // [stage][K|V][64][128B]
   const int lane = threadIdx.x & 63;
@@ -195,29 +208,41 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) qf[qb][ks] = *(const bf16x8_t*)(base + (size_t)q * ld + ks * 32 + 8 * g);
   }
+  if (!(flags & AACLIP_ATTN_Q_PRESCALED)) {  // log2(e)/sqrt(64) not folded by the caller: apply it here
+    constexpr float sl2 = 0.125f * 1.4426950408889634f;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (__bf16)((float)qf[qb][ks][e] * sl2);
+  }
 
   // ---- DMA sources: wave w loads pieces i*4+w (8 rows each) of the K and V tiles
-  int row_of_piece[2];
-  const uint16_t* ksrc[2];
-  const uint16_t* vsrc[2];
+  // through a buffer descriptor spanning this head's rows to the end of the batch:
+  // lane offsets are tile-invariant (VGPR), the tile step is a scalar offset, and
+  // keys past the last image read as zeros (keys past N inside the batch are the
+  // next image's finite rows; both are masked to p = 0 in the tail tile).
+  const int64_t head0 = (int64_t)b * N * ld + h * HD_;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(qkv + head0), 0, (int)(((int64_t)batch * N * ld - head0) * 2), 0x00020000);
+  int voff[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = (i * NW + wid) * 8 + (lane >> 3);
-    row_of_piece[i] = r;
     const int chunk = (lane & 7) ^ (r & 7);
-    ksrc[i] = base + HDt + chunk * 8;
-    vsrc[i] = base + 2 * HDt + chunk * 8;
+    voff[i] = (int)(r * ld + HDt + chunk * 8) * 2;
   }
+  const int row_bytes = (int)ld * 2, v_off = HDt * 2;
   auto stage = [&](int t, int buf) {
     char* kb = smem + buf * (2 * KT * 128);
     char* vb = kb + KT * 128;
+    const int so = t * KT * row_bytes;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int key = min(t * KT + row_of_piece[i], N - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(ksrc[i] + (size_t)key * ld),
-                                       LDS_PTR(kb + (i * NW + wid) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(vsrc[i] + (size_t)key * ld),
-                                       LDS_PTR(vb + (i * NW + wid) * 1024), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(kb + (i * NW + wid) * 1024), 16, voff[i], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(vb + (i * NW + wid) * 1024), 16, voff[i], so + v_off,
+                                               0, 0);
     }
   };
 
@@ -226,7 +251,7 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
     for (int db = 0; db < 4; ++db) ot[qb][db] = float4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-INFINITY, -INFINITY};
+  float m_run[2] = {0.f, 0.f};  // set from the first tile (attn_tile first = true)
   float4_t l_acc[2] = {float4_t{0.f, 0.f, 0.f, 0.f}, float4_t{0.f, 0.f, 0.f, 0.f}};  // row sums (MFMA)
 
   int ntiles = (N + KT - 1) / KT;
@@ -261,7 +286,8 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   for (; t < nfull; ++t) {
     const bool deep = advance();
     if (active)
-      attn_tile<4, 2, false>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g, c);
+      attn_tile<4, 2, false>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g, c,
+                             t == 0);
     if (deep) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
     cur = cur + 1 == NS ? 0 : cur + 1;
   }
@@ -271,9 +297,10 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     const int key0 = t * KT;
     const int live = min(KT, N - key0);  // valid keys in this tile
     if (active) {
-      if (live > 32) attn_tile<4, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c);
-      else if (live > 16) attn_tile<2, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c);
-      else attn_tile<1, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c);
+      const bool first = t == 0;
+      if (live > 32) attn_tile<4, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
+      else if (live > 16) attn_tile<2, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
+      else attn_tile<1, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
     }
     if (deep) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
     cur = cur + 1 == NS ? 0 : cur + 1;
@@ -418,20 +445,23 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(const float* __restrict__ 
 }  // namespace
 
 extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
-                                int heads, int head_dim, int causal, void* out_mx, int64_t ld_mx,
+                                int heads, int head_dim, int flags, void* out_mx, int64_t ld_mx,
                                 void* stream) {
   AACLIP_REQUIRE(dtype == AACLIP_F32 || dtype == AACLIP_BF16 || dtype == AACLIP_FP8);
   AACLIP_REQUIRE(qkv && out && batch > 0 && seq > 0 && heads > 0 && head_dim == HD_);
+  AACLIP_REQUIRE((flags & ~(AACLIP_ATTN_CAUSAL | AACLIP_ATTN_Q_PRESCALED)) == 0);
+  AACLIP_REQUIRE(dtype != AACLIP_F32 || !(flags & AACLIP_ATTN_Q_PRESCALED));
+  AACLIP_REQUIRE((int64_t)batch * seq * 3 * heads * HD_ * 2 < (1ll << 31));  // buffer-descriptor range
   AACLIP_REQUIRE(dtype != AACLIP_FP8 || (out_mx && ld_mx >= (int64_t)batch * seq && heads % 2 == 0));
   hipStream_t s = (hipStream_t)stream;
   if (dtype != AACLIP_F32) {  // bf16 compute; fp8 = bf16 inputs with an MX e4m3 output
     const long nwg = (long)ceil_div(seq, QT) * batch * heads;
     AACLIP_REQUIRE(nwg < (1L << 31));
-    attn_bf16_kernel<<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, seq, heads, causal,
-                                                   dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr, ld_mx);
+    attn_bf16_kernel<<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, batch, seq, heads,
+                                                   flags, dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr, ld_mx);
   } else {
     dim3 grid(ceil_div(seq, 64), batch * heads);
-    attn_f32_kernel<<<grid, 64, 0, s>>>((const float*)qkv, (float*)out, seq, heads, causal);
+    attn_f32_kernel<<<grid, 64, 0, s>>>((const float*)qkv, (float*)out, seq, heads, flags & AACLIP_ATTN_CAUSAL);
   }
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;

@@ -135,14 +135,20 @@ int aaclip_set_gemm_variant(int variant);
  * (scores never materialised). qkv: [batch*seq, 3*heads*head_dim] packed
  * [q|k|v] exactly as nn.MultiheadAttention's in_proj output; out:
  * [batch*seq, heads*head_dim] (heads merged, ready for out_proj).
- * causal != 0 adds the text tower's -inf upper triangle
- * (transformer.py:629-635). head_dim must be 64.
+ * flags: AACLIP_ATTN_CAUSAL adds the text tower's -inf upper triangle
+ * (transformer.py:629-635); AACLIP_ATTN_Q_PRESCALED (bf16/fp8 only) says the q
+ * columns already carry log2(e)/sqrt(head_dim) (folded into the Q projection
+ * weights and bias, so the kernel's softmax runs in the log2 domain with no
+ * per-score scaling); without it the kernel scales its Q fragments itself.
+ * head_dim must be 64.
  * Replaces: torch F.multi_head_attention_forward's q-scale/bmm/softmax/bmm
  * (transformer.py:200, need_weights=True branch; the averaged weights are
  * discarded by the caller, model/adapter.py:91 — never computed here).
  */
+#define AACLIP_ATTN_CAUSAL 1
+#define AACLIP_ATTN_Q_PRESCALED 2
 int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
-                     int heads, int head_dim, int causal, void* out_mx, int64_t ld_mx,
+                     int heads, int head_dim, int flags, void* out_mx, int64_t ld_mx,
                      void* stream);
 /* dtype AACLIP_FP8: bf16 qkv in, out written as MX e4m3 [batch*seq, heads*64] with one
  * e8m0 scale per (row, head) in out_mx [heads/2][ld_mx >= batch*seq][2] (the out-proj

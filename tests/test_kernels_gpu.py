@@ -249,6 +249,56 @@ def test_attention_spiky_rows(dev):
         assert (out.double() - ref).abs().max().item() < (2e-2 if dt == torch.bfloat16 else 1e-5)
 
 
+SL2 = 0.125 * 1.4426950408889634  # log2(e)/sqrt(64), what the engine folds into the Q projection
+
+
+def _prescale_q(qkv, H):
+    """q columns * log2(e)/8 rounded to bf16 (the engine's folded weights give the same rounding
+    point); returns the prescaled tensor and the unscaled (double) q it represents."""
+    x = qkv.clone()
+    x[:, :H * 64] = (qkv[:, :H * 64].float() * SL2).bfloat16()
+    ref_in = x.double()
+    ref_in[:, :H * 64] /= SL2
+    return x, ref_in
+
+
+@pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (1, 1025, 16, False),
+                                          (2, 5, 2, False), (4, 130, 4, True)])
+def test_attention_bf16_q_prescaled(dev, B, N, H, causal):
+    """AACLIP_ATTN_Q_PRESCALED: q already in the log2 domain (engine default for bf16/fp8)."""
+    torch.manual_seed(B * N + H + 1)
+    qkv = (torch.randn(B * N, 3 * H * 64, device=dev) * 1.5).bfloat16()
+    x, ref_in = _prescale_q(qkv, H)
+    out = torch.empty(B * N, H * 64, device=dev, dtype=torch.bfloat16)
+    ops.attention(x, out, B, N, H, causal=causal, q_prescaled=True)
+    ref = _attn_ref(ref_in, B, N, H, causal)
+    err = (out.double() - ref).abs().max().item()
+    assert err < 3e-2, err
+
+
+def test_attention_deferred_max_paths(dev):
+    """The running max moves only when a tile beats it by > 2^8: a slowly rising key
+    norm (max creeps up ~2 log2-units per tile: deferred, p grows up to 256) and a
+    late spike (+35 log2-units: the rescale branch) both match the float64 softmax."""
+    B, N, H = 2, 577, 2
+    torch.manual_seed(3)
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev) * 0.1
+    qkv[:, :64] = 1.0  # head 0: every query = ones
+    ramp = torch.arange(N, device=dev, dtype=torch.float32).repeat(B) / N * 2.0
+    qkv[:, H * 64:H * 64 + 64] = ramp[:, None]  # head 0 keys: logits rise with the key index
+    qkv[500, H * 64 + 64:H * 64 + 128] = 3.0  # head 1, key 500: a late spike (head-1 queries are small)
+    qkv[:, 64:128] = 1.0
+    for pre in (False, True):
+        x = qkv.bfloat16()
+        ref_in = x.double()
+        if pre:
+            x, ref_in = _prescale_q(x, H)
+        out = torch.empty(B * N, H * 64, device=dev, dtype=torch.bfloat16)
+        ops.attention(x, out, B, N, H, q_prescaled=pre)
+        ref = _attn_ref(ref_in, B, N, H, False)
+        assert (out.double() - ref).abs().max().item() < 2e-2, pre
+
+
 # ----------------------------------------------------------------------------- rows
 def test_layernorm_vs_reference(dev, golden):
     o = golden["ops"]

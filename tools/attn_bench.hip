@@ -35,14 +35,14 @@ int main(int argc, char** argv) {
   if (hipMalloc(&dq, nq * 2) != hipSuccess || hipMalloc(&dout, no * 2) != hipSuccess) return 1;
   if (hipMemcpy(dq, h.data(), nq * 2, hipMemcpyHostToDevice) != hipSuccess) return 1;
   for (int i = 0; i < 5; ++i)
-    if (aaclip_attention(AACLIP_BF16, dq, dout, B, N, H, 64, 0, nullptr)) return 2;
+    if (aaclip_attention(AACLIP_BF16, dq, dout, B, N, H, 64, 0, nullptr, 0, nullptr)) return 2;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   float best = 1e30f;
   for (int r = 0; r < 3; ++r) {
     (void)hipEventRecord(e0, nullptr);
-    for (int i = 0; i < reps; ++i) aaclip_attention(AACLIP_BF16, dq, dout, B, N, H, 64, 0, nullptr);
+    for (int i = 0; i < reps; ++i) aaclip_attention(AACLIP_BF16, dq, dout, B, N, H, 64, 0, nullptr, 0, nullptr);
     (void)hipEventRecord(e1, nullptr);
     (void)hipEventSynchronize(e1);
     float ms = 0.f;
