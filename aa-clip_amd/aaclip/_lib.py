@@ -56,7 +56,9 @@ SIGNATURES = {
     "aaclip_bicubic_taps": [_I, _I, ctypes.POINTER(_I)],
     "aaclip_bicubic_plan": [_I, _I, _P, _P, _I],
     "aaclip_nearest_plan": [_I, _I, _P],
-    "aaclip_preprocess_images": [_P, _L, _L, _I, _I, _I, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P],
+    "aaclip_preprocess_images": [_P, _L, _L, _I, _I, _I, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P, ctypes.c_size_t,
+                                 _P],
+    "aaclip_preprocess_workspace": [_I, _I, _I, _I, ctypes.POINTER(ctypes.c_size_t)],
     "aaclip_resize_masks_nearest": [_P, _L, _L, _I, _I, _I, _P, _P, _I, _P, _P],
 }
 

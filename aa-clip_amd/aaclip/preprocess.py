@@ -79,7 +79,18 @@ class Preprocessor:
         if not dense or x.shape[0] > 65535:
             raise ValueError("pixel rows must be contiguous (row pitch may be padded); batch <= 65535")
 
-    def images(self, u8: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    def _workspace(self, B, H, W, dev):
+        n = ctypes.c_size_t()
+        call("aaclip_preprocess_workspace", B, H, W, self.S, ctypes.byref(n))
+        ws = self._plans.get(("ws", dev))
+        if ws is None or ws.numel() < n.value:
+            ws = torch.empty(max(n.value, 1), device=dev, dtype=torch.uint8)
+            self._plans[("ws", dev)] = ws
+        return ws, n.value
+
+    def images(self, u8: torch.Tensor, out: torch.Tensor | None = None, two_pass: bool = True) -> torch.Tensor:
+        """two_pass: horizontal pass into a uint8 intermediate (a cached workspace), then
+        the vertical pass (default, faster); False = one tiled kernel, no workspace."""
         self._check_u8(u8, 3)
         B, H, W, _ = u8.shape
         dev = u8.device
@@ -89,8 +100,10 @@ class Preprocessor:
             out = torch.empty(B, 3, self.S, self.S, device=dev, dtype=torch.float32)
         if out.shape != (B, 3, self.S, self.S) or out.dtype != torch.float32 or not out.is_contiguous():
             raise ValueError("out must be contiguous fp32 [B,3,S,S]")
+        ws, nbytes = self._workspace(B, H, W, dev) if two_pass else (None, 0)
         call("aaclip_preprocess_images", _ptr(u8), u8.stride(0), u8.stride(1), B, H, W, _ptr(xb), _ptr(xk), kx,
-             _ptr(yb), _ptr(yk), ky, self.S, ctypes.cast(self._ms, ctypes.c_void_p), _ptr(out), _stream())
+             _ptr(yb), _ptr(yk), ky, self.S, ctypes.cast(self._ms, ctypes.c_void_p), _ptr(out), _ptr(ws), nbytes,
+             _stream())
         return out
 
     def masks(self, u8: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

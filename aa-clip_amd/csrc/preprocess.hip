@@ -159,6 +159,125 @@ __global__ __launch_bounds__(NT) void bicubic_normalize_kernel(PrepArgs a) {
   }
 }
 
+// ---- two-pass path (default when the caller passes a workspace): full-occupancy
+// passes with no per-tile row overlap. B=32 1024^2 -> 336: H 91 us + V 33 us
+// (single tiled kernel: 152 us). H is VALU-bound (16 unpredicated taps x 3
+// channels of byte * int32 MACs per output; 4-byte LDS reads + v_alignbyte
+// instead of byte reads measured the same). Pass H resamples every source row into the
+// uint8 intermediate image tmp [B][in_h][S][3] (Pillow's clipped intermediate);
+// pass V runs the vertical taps out of tmp (L2-resident rows, each read by ~ky/scale
+// output rows) and writes the normalised CHW fp32 output.
+struct HArgs {
+  const uint8_t* src;
+  int64_t img_stride, pitch;
+  int in_h, in_w, S, rows;  // rows: source rows per workgroup
+  const int32_t *xb, *xk;
+  int kx, srow, tstride;    // tstride: bytes per intermediate row (S*3 rounded up to 16)
+  uint8_t* tmp;
+};
+
+constexpr int HK = 16;  // max taps held in registers by the horizontal pass (kx <= HK)
+
+// blockDim = 64 * ceil(S / 64): thread x owns output column x, its taps live in
+// registers for all the workgroup's rows; the rows are staged in LDS by aligned
+// dword loads (8 in flight per thread) and read back as bytes.
+// K taps per column, unpredicated: the plan zero-fills taps past each column's
+// count (and srow carries K*3 spare bytes), so the short columns add 0 * byte
+// instead of branching per tap (a per-lane `t < n` test serialised the LDS reads).
+template <int K>
+__global__ __launch_bounds__(1024) void resample_h_kernel(HArgs a) {
+  const int nt = blockDim.x;
+  extern __shared__ __attribute__((aligned(16))) uint8_t rows[];  // [rows][srow]
+  const int b = blockIdx.y;
+  const int r0 = blockIdx.x * a.rows, nr = min(a.rows, a.in_h - r0);
+  const uint8_t* img = a.src + (size_t)b * a.img_stride;
+  const int ndw = (a.in_w * 3 + 3 + 3) >> 2;
+  constexpr int U = 8;
+  const int total = nr * ndw;
+  for (int i0 = threadIdx.x; i0 < total; i0 += nt * U) {
+    uint32_t v[U];
+    int dst[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nt;
+      dst[u] = -1;
+      if (i < total) {
+        const int r = i / ndw, d = i - r * ndw;
+        const uintptr_t row = (uintptr_t)(img + (size_t)(r0 + r) * a.pitch);
+        const uintptr_t base = row & ~(uintptr_t)3;  // aligned dwords never cross a page
+        if ((int)(row - base) + a.in_w * 3 > d * 4) {
+          v[u] = *(const uint32_t*)(base + 4 * (uintptr_t)d);
+          dst[u] = r * a.srow + 4 * d;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (dst[u] >= 0) *(uint32_t*)(rows + dst[u]) = v[u];
+  }
+  __syncthreads();
+  const int x = threadIdx.x;
+  if (x < a.S) {
+    const int xmin = a.xb[2 * x];
+    int w[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) w[t] = t < a.kx ? a.xk[(size_t)x * a.kx + t] : 0;  // kx is uniform
+    for (int r = 0; r < nr; ++r) {
+      const uintptr_t row = (uintptr_t)(img + (size_t)(r0 + r) * a.pitch);
+      const uint8_t* p = rows + r * a.srow + (int)(row & 3) + xmin * 3;
+      int s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
+#pragma unroll
+      for (int t = 0; t < K; ++t) {
+        s0 += (int)p[3 * t + 0] * w[t];
+        s1 += (int)p[3 * t + 1] * w[t];
+        s2 += (int)p[3 * t + 2] * w[t];
+      }
+      uint8_t* d = a.tmp + ((size_t)b * a.in_h + r0 + r) * a.tstride + x * 3;
+      d[0] = (uint8_t)clip8(s0);
+      d[1] = (uint8_t)clip8(s1);
+      d[2] = (uint8_t)clip8(s2);
+    }
+  }
+}
+
+// one thread = 4 consecutive output pixels (12 intermediate bytes = 3 aligned
+// dwords per tap) of one output row; a 64-thread block covers 256 pixels and the
+// row's taps are block-uniform (scalar loads)
+__global__ __launch_bounds__(64) void resample_v_kernel(const uint8_t* __restrict__ tmp, int in_h, int S,
+                                                        int tstride, const int32_t* __restrict__ yb,
+                                                        const int32_t* __restrict__ yk, int ky, float m0,
+                                                        float m1, float m2, float s0_, float s1_, float s2_,
+                                                        float* __restrict__ out) {
+  const int b = blockIdx.z, y = blockIdx.y, x0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+  const int ymin = yb[2 * y], n = yb[2 * y + 1];
+  const int32_t* k = yk + (size_t)y * ky;
+  if (x0 >= S) return;
+  const uint8_t* col = tmp + ((size_t)b * in_h + ymin) * tstride + x0 * 3;
+  int acc[12];
+#pragma unroll
+  for (int e = 0; e < 12; ++e) acc[e] = 1 << (PREC - 1);
+#pragma unroll 2
+  for (int t = 0; t < n; ++t) {
+    const int w = k[t];
+    const uint32_t* q = (const uint32_t*)(col + (size_t)t * tstride);  // x0*3 % 12 == 0, tstride % 16 == 0
+    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[e] += (int)((d0 >> (8 * e)) & 255) * w;
+      acc[4 + e] += (int)((d1 >> (8 * e)) & 255) * w;
+      acc[8 + e] += (int)((d2 >> (8 * e)) & 255) * w;
+    }
+  }
+  const size_t plane = (size_t)S * S, o = (size_t)b * 3 * plane + (size_t)y * S + x0;
+  const float mean[3] = {m0, m1, m2}, sd[3] = {s0_, s1_, s2_};
+#pragma unroll
+  for (int px = 0; px < 4; ++px)
+    if (x0 + px < S)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        out[o + c * plane + px] = ((float)clip8(acc[3 * px + c]) / 255.0f - mean[c]) / sd[c];
+}
+
 __global__ __launch_bounds__(NT) void nearest_mask_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
                                                           int64_t pitch, const int32_t* __restrict__ xi,
                                                           const int32_t* __restrict__ yi, int S,
@@ -254,10 +373,28 @@ extern "C" int aaclip_nearest_plan(int in_size, int out_size, int32_t* index) {
   return AACLIP_OK;
 }
 
+namespace {
+int tmp_stride(int S) { return (S * 3 + 12 + 15) & ~15; }  // + 12: the last 4-pixel group's dwords
+constexpr int H_LDS = 64 * 1024;
+// bytes of LDS the horizontal pass needs for `rows` source rows (0 = does not fit)
+int h_lds_bytes(int in_w, int rows, int* srow) {
+  *srow = (in_w * 3 + 3 + 3 + 3 * HK + 8 + 15) & ~15;  // + 3*HK + 8: zero-weight taps / dword tail
+  const int64_t bytes = (int64_t)rows * *srow;
+  return bytes <= H_LDS ? (int)bytes : 0;
+}
+}  // namespace
+
+extern "C" int aaclip_preprocess_workspace(int batch, int in_h, int in_w, int out_size, size_t* bytes) {
+  AACLIP_REQUIRE(batch >= 0 && in_h > 0 && in_w > 0 && out_size > 0 && bytes);
+  *bytes = (size_t)batch * in_h * tmp_stride(out_size);  // the uint8 intermediate image of the two-pass path
+  return AACLIP_OK;
+}
+
 extern "C" int aaclip_preprocess_images(const uint8_t* src, int64_t img_stride, int64_t row_pitch, int batch,
                                         int in_h, int in_w, const int32_t* x_bounds, const int32_t* x_coeffs,
                                         int kx, const int32_t* y_bounds, const int32_t* y_coeffs, int ky,
-                                        int out_size, const float* mean_std, float* out, void* stream) {
+                                        int out_size, const float* mean_std, float* out, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
   AACLIP_REQUIRE(src && x_bounds && x_coeffs && y_bounds && y_coeffs && out && batch >= 0);
   AACLIP_REQUIRE(in_h > 0 && in_w > 0 && out_size > 0 && row_pitch >= (int64_t)in_w * 3);
   AACLIP_REQUIRE(img_stride >= row_pitch * in_h || batch <= 1);
@@ -284,7 +421,38 @@ extern "C" int aaclip_preprocess_images(const uint8_t* src, int64_t img_stride, 
     a.stdv[c] = ms[3 + c];
   }
   a.out = out;
-  // tile choice: the tallest/widest staged tile (from 16 x 32) whose weights + strip + patch
+  // two-pass path: needs the caller's workspace and the source rows + tap table in LDS
+  int srow = 0, hrows = 8, hlds = 0;
+  if (const char* e = getenv("AACLIP_PREP_HROWS")) hrows = std::max(1, atoi(e));  // tuning
+  while (hrows > 0 && !(hlds = h_lds_bytes(in_w, hrows, &srow))) hrows >>= 1;
+  const int tstride = tmp_stride(out_size);
+  if (workspace && workspace_bytes >= (size_t)batch * in_h * tstride && hlds && kx <= HK && out_size <= 1024 &&
+      batch <= 65535 &&
+      !getenv("AACLIP_PREP_TILE")) {
+    static bool h_attr = false;  // benign race: idempotent attribute writes
+    if (!h_attr) {
+      if (hipFuncSetAttribute((const void*)resample_h_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              H_LDS) != hipSuccess ||
+          hipFuncSetAttribute((const void*)resample_h_kernel<HK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              H_LDS) != hipSuccess)
+        return AACLIP_ERR_LAUNCH;
+      h_attr = true;
+    }
+    HArgs h{src, img_stride, row_pitch, in_h, in_w, out_size, hrows, x_bounds, x_coeffs, kx, srow, tstride,
+            (uint8_t*)workspace};
+    const dim3 hgrid(ceil_div(in_h, hrows), batch);
+    if (kx <= 8)
+      resample_h_kernel<8><<<hgrid, 64 * ceil_div(out_size, 64), hlds, (hipStream_t)stream>>>(h);
+    else
+      resample_h_kernel<HK><<<hgrid, 64 * ceil_div(out_size, 64), hlds, (hipStream_t)stream>>>(h);
+    AACLIP_CHECK_LAUNCH();
+    resample_v_kernel<<<dim3(ceil_div(out_size, 256), out_size, batch), 64, 0, (hipStream_t)stream>>>(
+        (const uint8_t*)workspace, in_h, out_size, tstride, y_bounds, y_coeffs, ky, a.mean[0], a.mean[1],
+        a.mean[2], a.stdv[0], a.stdv[1], a.stdv[2], out);
+    AACLIP_CHECK_LAUNCH();
+    return AACLIP_OK;
+  }
+  // single-kernel path (no workspace, or rows too wide for LDS): tile choice: the tallest/widest staged tile (from 16 x 32) whose weights + strip + patch
   // fit STAGED_LDS, else direct taps. 1024 -> 336: 16 x 32 tiles, 62 x 111-pixel patches,
   // 32 KB -> 4 workgroups per CU. Measured at B=32 1024^2 (tools/prep_sweep.sh):
   // 16x64 257 us, 8x64 195, 16x32 152, 16x16 144, direct 257 -- occupancy-bound.

@@ -314,7 +314,13 @@ int aaclip_nearest_plan(int in_size, int out_size, int32_t* index);
 int aaclip_preprocess_images(const uint8_t* src, int64_t img_stride, int64_t row_pitch, int batch,
                              int in_h, int in_w, const int32_t* x_bounds, const int32_t* x_coeffs,
                              int kx, const int32_t* y_bounds, const int32_t* y_coeffs, int ky,
-                             int out_size, const float* mean_std, float* out, void* stream);
+                             int out_size, const float* mean_std, float* out, void* workspace,
+                             size_t workspace_bytes, void* stream);
+/* workspace (optional, caller-owned device memory of aaclip_preprocess_workspace
+ * bytes): enables the two-pass path (horizontal pass into a uint8 intermediate,
+ * then the vertical pass); NULL = one tiled kernel with no intermediate. Same
+ * output bits either way. */
+int aaclip_preprocess_workspace(int batch, int in_h, int in_w, int out_size, size_t* bytes);
 
 /*
  * src: batch uint8 L masks [in_h, in_w]; out fp32 [batch, 1, S, S] =

@@ -105,10 +105,12 @@ def test_preprocess_rejects_bad_calls():
     f16 = ctypes.c_void_p(16)
     # row pitch smaller than a row of RGB pixels
     assert lib.aaclip_preprocess_images(f16, 900 * 900 * 3, 899 * 3, 1, 900, 900, f16, f16, 13, f16, f16, 13, 336,
-                                        None, f16, None) == 1
+                                        None, f16, None, 0, None) == 1
     # plan narrower than the resampling support
     assert lib.aaclip_preprocess_images(f16, 900 * 900 * 3, 900 * 3, 1, 900, 900, f16, f16, 5, f16, f16, 13, 336,
-                                        None, f16, None) == 1
+                                        None, f16, None, 0, None) == 1
+    n = ctypes.c_size_t()
+    assert lib.aaclip_preprocess_workspace(4, 900, 700, 336, ctypes.byref(n)) == 0 and n.value >= 4 * 900 * 336 * 3
     assert lib.aaclip_resize_masks_nearest(None, 0, 900, 1, 900, 900, f16, f16, 336, f16, None) == 1
 
 
@@ -122,8 +124,10 @@ def test_device_preprocess_bit_exact(dev, H, W, S):
     masks = np.stack([_mask(H, W, S + i) for i in range(B)])
     pp = Preprocessor(S)
     out = pp.images(torch.from_numpy(imgs).to(dev))
+    one = pp.images(torch.from_numpy(imgs).to(dev), two_pass=False)
     mo = pp.masks(torch.from_numpy(masks).to(dev))
     torch.cuda.synchronize()
+    assert torch.equal(out, one)  # two-pass and single-kernel paths: same bits
     for i in range(B):
         assert np.array_equal(out[i].cpu().numpy(), P.transform_image(imgs[i], S)), i
         assert np.array_equal(mo[i].cpu().numpy(), P.transform_mask(masks[i], S)), i
@@ -143,8 +147,9 @@ def test_device_preprocess_padded_pitch_and_batch_stride(dev):
         stage = stage.to(dev)
         view = stage[:, :H, off:off + W * 3].unflatten(2, (W, 3))
         assert view.stride(1) == pitch + off and view.stride(0) == (H + 3) * (pitch + off)
-        out = Preprocessor(S).images(view)
-        assert torch.equal(out, ref), (pitch, off)
+        for two in (True, False):
+            out = Preprocessor(S).images(view, two_pass=two)
+            assert torch.equal(out, ref), (pitch, off, two)
     assert np.array_equal(ref[2].cpu().numpy(), P.transform_image(imgs[2], S))
 
 
