@@ -99,6 +99,32 @@ def time_launches(fn, reps, stream):
     return start.elapsed_time(end) / reps  # ms per launch
 
 
+def preprocess_leg(dev, batch, size, reps=20):
+    """SURVEY 8(f)-3 on device: B decoded uint8 RGB images (1024x1024, MVTec's size)
+    -> Pillow-exact BICUBIC resize + ToTensor + Normalize -> fp32 [B,3,S,S]
+    (aaclip_preprocess_images, two-pass), and the NEAREST mask resize. HIP events
+    on the launch stream; algorithmic bytes = B*H*W*3 read + B*3*S*S*4 written."""
+    from aaclip.preprocess import Preprocessor
+    H = W = 1024
+    g = torch.Generator(device=dev).manual_seed(5)
+    u8 = torch.randint(0, 256, (batch, H, W, 3), device=dev, dtype=torch.uint8, generator=g)
+    m8 = (torch.rand(batch, H, W, device=dev, generator=g) < 0.05).to(torch.uint8)
+    pp = Preprocessor(size)
+    out = torch.empty(batch, 3, size, size, device=dev)
+    mo = torch.empty(batch, 1, size, size, device=dev)
+    st = torch.cuda.current_stream()
+    t_img = time_launches(lambda: pp.images(u8, out), reps, st)
+    t_mask = time_launches(lambda: pp.masks(m8, mo), reps, st)
+    alg = batch * H * W * 3 + batch * 3 * size * size * 4
+    gbs = alg / (t_img * 1e-3) / 1e9
+    return {"workload": f"{batch} x {H}x{W} uint8 RGB -> fp32 [{batch},3,{size},{size}] (Pillow BICUBIC exact)",
+            "images_per_sec": round(batch / (t_img * 1e-3), 1), "us_per_batch": round(t_img * 1e3, 1),
+            "mask_us_per_batch": round(t_mask * 1e3, 1),
+            "roofline": {"kernel": "resample_h_kernel + resample_v_kernel", "bound": "hbm", "unit": "GB/s",
+                         "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes_per_launch": alg, "traffic": None}}
+
+
 def roofline_gemm(eng, ws, reps=20):
     """Dominant kernel = bf16 MFMA GEMM <320x256> (QKV and c_fc launches).
     Average HIP-event launch duration over the two shapes it runs at."""
@@ -364,6 +390,8 @@ def main():
         line["roofline_map"] = roofline_map(eng, ws, T)
     if rank == 0 and world == 1 and args.cpu_images > 0:
         line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(args.cpu_images, dev, args.streams)
+    if rank == 0 and world == 1 and not args.no_roofline:
+        line["preprocess"] = preprocess_leg(dev, B, S)
     if rank == 0 and world == 1 and not args.no_c5:
         del eng, run
         torch.cuda.empty_cache()
