@@ -114,8 +114,9 @@ def gemm_fp8(a: torch.Tensor, a_scale: torch.Tensor, w: torch.Tensor, w_scale: t
 
 def mx_scales(rows: int, cols: int, device, ld: int = None) -> torch.Tensor:
     """e8m0 scale buffer of an MX fp8 tensor [rows, cols]: [cols/128, ld, 2] uint8
-    (one byte per (row, 64-column block); the two blocks of a 128-K step adjacent)."""
-    return torch.empty(cols // 128, ld or rows, 2, device=device, dtype=torch.uint8)
+    (one byte per (row, 64-column block); the two blocks of a 128-K step adjacent).
+    ld defaults to rows rounded up to even (the MX GEMM moves scales as dwords)."""
+    return torch.empty(cols // 128, ld or (rows + 1) // 2 * 2, 2, device=device, dtype=torch.uint8)
 
 
 def quant_fp8_mx(x: torch.Tensor, q: torch.Tensor, sc: torch.Tensor) -> None:
@@ -145,8 +146,9 @@ def gemm_fp8mx(a: torch.Tensor, a_sc: torch.Tensor, w: torch.Tensor, w_scale: to
     N = w.shape[0]
     if w.shape[1] != K or out.shape[1] != N or out.shape[0] < M or w_scale.numel() != N:
         raise ValueError(f"gemm_fp8mx shape mismatch a{tuple(a.shape)} w{tuple(w.shape)} out{tuple(out.shape)}")
-    if a_sc.dtype != torch.uint8 or a_sc.dim() != 3 or a_sc.shape[0] != K // 128 or a_sc.shape[1] < M:
-        raise ValueError("a_sc must be uint8 [K/128, ld >= M, 2]")
+    if a_sc.dtype != torch.uint8 or a_sc.dim() != 3 or a_sc.shape[0] != K // 128 or a_sc.shape[1] < M or \
+            a_sc.shape[1] % 2:
+        raise ValueError("a_sc must be uint8 [K/128, ld >= M (even), 2]")
     if out.dtype == FP8:
         if out_sc is None or out_sc.shape[0] != N // 128 or out_sc.shape[1] < M:
             raise ValueError("fp8 output needs out_sc uint8 [N/128, ld >= M, 2]")

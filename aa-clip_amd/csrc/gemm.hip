@@ -996,7 +996,11 @@ extern "C" int aaclip_gemm_fp8mx(int out_dtype, int M, int N, int K, const void*
                                  void* aux, int64_t ldaux, void* c_mx, int64_t ld_cmx, void* stream) {
   AACLIP_REQUIRE(out_dtype == AACLIP_F32 || out_dtype == AACLIP_BF16 || out_dtype == AACLIP_FP8);
   AACLIP_REQUIRE(A && W && C && a_mx && w_scale && M >= 0 && N > 0 && K > 0);
-  AACLIP_REQUIRE(K % 128 == 0 && N % 256 == 0 && ld_amx >= M);
+  // ld_amx even: the scale DMA moves dwords, and with an odd ld the K-step bases sit at
+  // 2 mod 4 bytes, so the last row's dword in the last K-step straddles the buffer
+  // end and the range check drops it (scale 0 -> that row wrong; found by the
+  // batch-composition invariance test at odd image counts)
+  AACLIP_REQUIRE(K % 128 == 0 && N % 256 == 0 && ld_amx >= M && ld_amx % 2 == 0);
   AACLIP_REQUIRE(lda >= K && ldw >= K && ldc >= N && lda % 16 == 0 && ldw % 16 == 0 && ldc % 16 == 0);
   AACLIP_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0 && ((uintptr_t)C % 16) == 0);
   AACLIP_REQUIRE(((uintptr_t)w_scale % 16) == 0 && ((uintptr_t)a_mx % 4) == 0);

@@ -93,7 +93,7 @@ int aaclip_gemm_fp8(int out_dtype, int M, int N, int K, const void* A, int64_t l
  * out_dtype AACLIP_FP8 (only with bias+GELU, the c_fc -> c_proj hand-off): C is
  * written as e4m3 with its own e8m0 scale per (row, 64 columns) in c_mx
  * [N/128][ld_cmx][2], ready to be the A operand of the next MX GEMM.
- * K % 128 == 0, N % 256 == 0, ld_amx >= M.
+ * K % 128 == 0, N % 256 == 0, ld_amx >= M and even (the scales move as dwords).
  */
 int aaclip_gemm_fp8mx(int out_dtype, int M, int N, int K, const void* A, int64_t lda,
                       const void* a_mx, int64_t ld_amx, const void* W, int64_t ldw,

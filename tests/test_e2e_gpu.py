@@ -155,3 +155,26 @@ def test_graphed_predict_matches_eager(dev, weights):
         m2 = m2.clone()
         m3, _ = eng.predict(x2, T, "Industrial", streams=streams)
         assert torch.equal(m2, m3)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float8_e4m3fn])
+def test_batch_composition_invariance(dev, weights, dtype):
+    """Images are independent units: every per-row kernel (GEMM rows, LayerNorm rows,
+    per-(image, head) attention, per-image maps/scores) computes the same bits for an
+    image whatever the batch size, its position in the batch and the stream chunking
+    (size-independent property backing the B=32 bench line and the image sharding)."""
+    eng = _visual(weights, dtype)
+    g = torch.Generator(device=dev).manual_seed(9)
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
+    x = torch.randn(7, 3, 336, 336, device=dev, generator=g)
+    ref_m, ref_s = [], []
+    for i in range(7):
+        m, s = eng.predict(x[i:i + 1], T, "Industrial", streams=1)
+        ref_m.append(m.clone())
+        ref_s.append(s.clone())
+    ref_m, ref_s = torch.cat(ref_m), torch.cat(ref_s)
+    for B, streams in ((7, 1), (7, 2), (7, 3), (5, 2), (3, 4)):
+        idx = torch.arange(7 - B, 7, device=dev) if B == 5 else torch.arange(B, device=dev)
+        m, s = eng.predict(x[idx], T, "Industrial", streams=streams)
+        assert torch.equal(m, ref_m[idx]), (B, streams)
+        assert torch.equal(s, ref_s[idx]), (B, streams)

@@ -175,7 +175,7 @@ def test_gemm_fp8mx(dev, mx_variant, M, N, K):
     a = torch.randn(M, K, device=dev) * torch.logspace(-2, 2, K // 64, device=dev).repeat_interleave(64)
     w = torch.randn(N, K, device=dev) * K ** -0.5
     a8 = torch.empty(M, K, device=dev, dtype=FP8)
-    asc = ops.mx_scales(M, K, dev, ld=M + 5)
+    asc = ops.mx_scales(M, K, dev, ld=(M + 7) // 2 * 2)  # padded, even
     ops.quant_fp8_mx(a, a8, asc)
     w8, sw = _wq(w)
     bias = torch.randn(N, device=dev) * 0.1
@@ -187,6 +187,30 @@ def test_gemm_fp8mx(dev, mx_variant, M, N, K):
     scale = A.abs() @ Wd.abs().T
     err = (out.double() - ref).abs()
     assert (err <= 3e-5 * scale + 1e-6).all(), (err / scale).max().item()
+
+
+@pytest.mark.parametrize("M", [1025, 7175, 1, 255])
+def test_gemm_fp8mx_odd_rows_last_row(dev, mx_variant, M):
+    """Odd row counts (one image = 1025 tokens): the last row's scales sit at the very
+    end of the scale buffer; with the (even-padded) default ld every row is exact,
+    and an odd ld is rejected (the dword scale DMA would drop the last row's scale)."""
+    torch.manual_seed(M)
+    K, N = 1024, 1024
+    a = torch.randn(M, K, device=dev)
+    a8 = torch.empty(M, K, device=dev, dtype=FP8)
+    asc = ops.mx_scales(M, K, dev)
+    ops.quant_fp8_mx(a, a8, asc)
+    w8, sw = _wq(torch.randn(N, K, device=dev) * K ** -0.5)
+    out = torch.empty(M, N, device=dev)
+    ops.gemm_fp8mx(a8, asc, w8, sw, out)
+    ref = _mx_dequant(a8, asc) @ (w8.double() * sw.double()[:, None]).T
+    err = (out.double() - ref).abs().amax(1)
+    assert (err <= 1e-3).all(), err.argmax().item()
+    if M % 2:
+        odd = ops.mx_scales(M, K, dev, ld=M)
+        ops.quant_fp8_mx(a, a8, odd)
+        with pytest.raises(ValueError):
+            ops.gemm_fp8mx(a8, odd, w8, sw, out)
 
 
 def test_gemm_fp8mx_gelu_fp8_output_chain(dev, mx_variant):
@@ -258,7 +282,7 @@ def test_layernorm_kernels_mx_output(dev):
     q = torch.empty(R, W, device=dev, dtype=FP8)
     s = ops.mx_scales(R, W, dev)
     ops.layernorm(x, w, b, q, y_sc=s)
-    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8)) and torch.equal(s, s_ref)
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8)) and torch.equal(s[:, :R], s_ref[:, :R])
     # block tail: adapter blend + next ln_1 (MX) + bf16 tap
     u = torch.randn(R, W, device=dev)
     post = (torch.randn(W, device=dev), torch.randn(W, device=dev))
@@ -269,7 +293,7 @@ def test_layernorm_kernels_mx_output(dev):
     ops.block_tail(x1, n_tok, u=u, adapt_weight=0.1, ln=(w, b), h=h32, post=post, tap=None)
     ops.block_tail(x2, n_tok, u=u, adapt_weight=0.1, ln=(w, b), h=q, post=post, tap=tap2, h_sc=s)
     ops.quant_fp8_mx(h32, q_ref, s_ref)
-    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8)) and torch.equal(s, s_ref)
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8)) and torch.equal(s[:, :R], s_ref[:, :R])
     ops.block_tail(x.clone(), n_tok, u=u, adapt_weight=0.1, ln=None, h=None, post=post, tap=tap1)
     assert torch.equal(tap1, tap2)
 
@@ -313,4 +337,5 @@ def test_attention_mx_output_not_worse_than_requantised_bf16(dev):
     e_new = (_mx_dequant(o8, sc) - o32.double()).abs().mean().item()
     e_old = (_mx_dequant(r8, rsc) - o32.double()).abs().mean().item()
     assert e_new <= e_old * 1.01, (e_new, e_old)
+    sc, rsc = sc[:, :B * N], rsc[:, :B * N]  # the even-ld pad row is never written
     assert torch.equal(sc, rsc) or (sc.int() - rsc.int()).abs().max().item() <= 1
