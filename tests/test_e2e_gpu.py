@@ -178,3 +178,18 @@ def test_batch_composition_invariance(dev, weights, dtype):
         m, s = eng.predict(x[idx], T, "Industrial", streams=streams)
         assert torch.equal(m, ref_m[idx]), (B, streams)
         assert torch.equal(s, ref_s[idx]), (B, streams)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_text_encode_sequence_invariance(dev, golden, weights, dtype):
+    """Prompts are independent sequences: encoding 10 prompts at once gives each the
+    same bits as encoding it alone or inside an odd-sized subset (causal attention
+    per sequence, row-independent GEMM / LayerNorm rows)."""
+    sd, _, ta, _ = weights
+    tp = {k: v for k, v in sd.items() if not k.startswith("visual.")}
+    eng = TextEngine(tp, ta, dtype=dtype)
+    tok = torch.from_numpy(golden["text"]["bottle_tok_abnormal"]).to(dev)
+    full = eng.encode(tok).clone()
+    for i in (0, 4, tok.shape[0] - 1):
+        assert torch.equal(eng.encode(tok[i:i + 1]), full[i:i + 1]), i
+    assert torch.equal(eng.encode(tok[3:6]), full[3:6])
