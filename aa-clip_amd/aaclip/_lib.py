@@ -38,6 +38,7 @@ SIGNATURES = {
     "aaclip_gemm_fp8mx": [_I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _P, _P, _L, _P, _L, _P, _L, _P],
     "aaclip_quant_fp8_mx": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _P],
     "aaclip_set_gemm_variant": [_I],
+    "aaclip_gemm_plan": [_I, _I, _I, _I],
     "aaclip_attention": [_I, _P, _P, _I, _I, _I, _I, _I, _P, _L, _P],
     "aaclip_im2col": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "aaclip_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],
@@ -77,7 +78,7 @@ def lib() -> ctypes.CDLL:
         for name, argtypes in SIGNATURES.items():
             fn = getattr(handle, name)
             fn.argtypes = argtypes
-            fn.restype = ctypes.c_char_p if name == "aaclip_arch" else ctypes.c_int
+            fn.restype = ctypes.c_char_p if name in ("aaclip_arch", "aaclip_gemm_plan") else ctypes.c_int
         if handle.aaclip_abi_version() != ABI_VERSION:
             raise RuntimeError("libaaclip_hip.so ABI version mismatch; rebuild it")
         _lib = handle

@@ -900,18 +900,57 @@ int launch_bf16(GemmArgs a, hipStream_t s) {
 
 
 int g_gemm_variant = 0;  // tuning hook (aaclip_set_gemm_variant); 0 = default dispatch
+
+int cu_count() {
+  static int n[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
+  if (!n[dev] && hipDeviceGetAttribute(&n[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    n[dev] = 256;  // benign race: idempotent
+  return n[dev] > 0 ? n[dev] : 256;
+}
+
+// tile rounds x tile rows, 8-phase 256-row tiles weighted 10/11 for their faster main loop
+bool prefer_8ph(int M, int N) {
+  const int cus = cu_count();
+  const int64_t t320 = (int64_t)ceil_div(M, 320) * (N / 256), t256 = (int64_t)ceil_div(M, 256) * (N / 256);
+  const int64_t c320 = ((t320 + cus - 1) / cus) * 320 * 11, c256 = ((t256 + cus - 1) / cus) * 256 * 10;
+  return c256 < c320;
+}
 int g_group_m = 8;
 int g_setprio = 0;
 int g_dbg = 0;
 
 }  // namespace
 
+// Which kernel aaclip_gemm launches for this shape (same decision as the dispatch
+// below; for reports such as bench.py's roofline label). Host only.
+extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
+  if (in_dtype != AACLIP_BF16) return "gemm_f32_kernel";
+  if (M <= 0 || N % 128 || K % 64) return "invalid";
+  switch (g_gemm_variant) {
+    case 1: return "gemm_bf16_kernel<256,256,2,4>";
+    case 2: return "gemm_bf16_kernel<256,128,4,2>";
+    case 3:
+    case 4:
+      if (N % 256 == 0 && (g_gemm_variant == 3 || N >= 2048)) return "gemm_bf16_8ph_kernel<256,256>";
+      break;
+    case 8:
+      if (N % 256 == 0) return "gemm_bf16_kernel<320,256,2,4>";
+      break;
+    default: break;
+  }
+  if (N % 256 == 0 && g_gemm_variant == 0 && prefer_8ph(M, N)) return "gemm_bf16_8ph_kernel<256,256>";
+  return N % 256 == 0 ? "gemm_bf16_kernel<320,256,2,4>" : "gemm_bf16_kernel<256,128,4,2>";
+}
+
 extern "C" int aaclip_set_gemm_variant(int variant) {
-  // bits 0-3: tile family (0 default, 1 = 256x256, 2 = 256x128, 3/4 = 256x256 8-phase ping-pong,
-  // 6 = MX fp8 on the 256x256 LDS-DMA kernel instead of its 8-phase default); bits 4-7: tile-order
+  // bits 0-3: tile family (0 default = per-shape choice, 1 = 256x256, 2 = 256x128, 3/4 = 256x256
+  // 8-phase ping-pong everywhere / for N >= 2048, 6 = MX fp8 on the 256x256 LDS-DMA kernel instead
+  // of its 8-phase default, 8 = 320x256 everywhere); bits 4-7: tile-order
   // group height (0 = 8); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 2048 || fam > 6 || fam == 5) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 2048 || fam > 8 || fam == 5 || fam == 7) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 8;
   g_setprio = (variant >> 8) & 1;
@@ -950,11 +989,20 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
             (int64_t)N * ldw * 2 < (1ll << 31))
           return launch_bf16_8ph(a, s);
         break;
+      case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
+        if (N % 256 == 0) return launch_bf16<320, 256, 2, 4>(a, s);
+        break;
       default: break;
     }
-    // M = B*577 tiles badly by 256 (18464 = 72.1 x 256 at B=32: 3.42 waves of 256x256
-    // tiles for N=3072, 1.14 for N=1024); 320-row tiles give 58 M-tiles -> 0.91 / 2.72 /
-    // 3.63 waves for N = 1024 / 3072 / 4096 (measured 1.1-1.4x faster on every block GEMM).
+    // Default: per shape, the kernel with the fewer tile rounds weighted by its per-tile
+    // cost. M = B*577 tiles unevenly: 320-row tiles of the LDS-DMA kernel vs 256-row
+    // tiles of the 8-phase kernel (~10 % faster per FLOP). E.g. in the two-stream
+    // pipeline (16 images per stream, M = 9232) the 8-phase kernel wins on QKV, out-proj,
+    // c_proj and adapters (148-444 tiles) and the 320-row one on c_fc (464 vs 592 tiles
+    // = 2 vs 3 rounds); measured per shape with tools/kbench.py, whole C2 step +5 %.
+    if (N % 256 == 0 && g_gemm_variant == 0 && (int64_t)M * lda * 2 < (1ll << 31) &&
+        (int64_t)N * ldw * 2 < (1ll << 31) && prefer_8ph(M, N))
+      return launch_bf16_8ph(a, s);
     if (N % 256 == 0) return launch_bf16<320, 256, 2, 4>(a, s);
     return launch_bf16<256, 128, 4, 2>(a, s);
   }

@@ -126,8 +126,9 @@ def preprocess_leg(dev, batch, size, reps=20):
 
 
 def roofline_gemm(eng, ws, reps=20):
-    """Dominant kernel = bf16 MFMA GEMM <320x256> (QKV and c_fc launches).
-    Average HIP-event launch duration over the two shapes it runs at."""
+    """Dominant kernel = the bf16 MFMA GEMM (QKV and c_fc launches; which tile family
+    the per-shape dispatch picks is reported). Average HIP-event launch duration over
+    the two shapes."""
     s = torch.cuda.current_stream()
     blk = eng.blocks[0]
     R = ws["x"].shape[0]
@@ -147,8 +148,11 @@ def roofline_gemm(eng, ws, reps=20):
     block_flops = f_qkv + f_fc + 2.0 * R * WIDTH * WIDTH + 2.0 * R * 4 * WIDTH * WIDTH + f_at
     block_ms = t_qkv + t_fc + t_o + t_pr + t_at
     traffic, src = pmc_traffic("gemm")
+    from aaclip import _lib
+    k_qkv = _lib.lib().aaclip_gemm_plan(_lib.BF16, R, 3 * WIDTH, WIDTH).decode()
+    k_fc = _lib.lib().aaclip_gemm_plan(_lib.BF16, R, 4 * WIDTH, WIDTH).decode()
     return {
-        "kernel": "gemm_bf16_kernel<320,256,2,4> (QKV + c_fc launches)",
+        "kernel": f"{k_qkv} (QKV) + {k_fc} (c_fc) at M = {R}",
         "bound": "mfma", "unit": "TFLOP/s", "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS,
         "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_source": src,
         "algorithmic_bytes_per_launch": (R * WIDTH * 2 + 3 * WIDTH * WIDTH * 2 + R * 3 * WIDTH * 2

@@ -47,9 +47,10 @@ if __name__ == "__main__":
     a = ap.parse_args()
     s = summarise(a.root)
     if a.traffic_out:
-        # C2 (B=32): QKV grid 58x12 and c_fc grid 58x16 workgroups of 512 threads
-        gemm = [e for e in s if "gemm_bf16_kernel<320" in e["kernel"] and e["grid_size"] in (696 * 512, 928 * 512)
-                and "hbm_bytes" in e]
+        # C2 (B=32, M = 18464): QKV and c_fc launches of 512-thread workgroups, on the
+        # 320x256 kernel (58 x 12 / 58 x 16 tiles) or the 8-phase 256x256 one (73 x 12 / 73 x 16)
+        grids = {696 * 512, 928 * 512, 876 * 512, 1168 * 512}
+        gemm = [e for e in s if "gemm_bf16" in e["kernel"] and e["grid_size"] in grids and "hbm_bytes" in e]
         mp = [e for e in s if "patch_scores" in e["kernel"] and "hbm_bytes" in e]
         t = {"source": f"rocprofv3 --pmc passes (tools/prof_pmc.sh) summarised by tools/pmc_summary.py from {a.root}; "
                        "read = FETCH_SIZE*1024*2 (gfx950 half-count correction), write = WRITE_SIZE*1024"}
