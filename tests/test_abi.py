@@ -58,3 +58,21 @@ def test_product_path_does_not_import_the_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, flags=re.M), f
+
+
+def test_gemm_plan_per_shape_choice():
+    """The default bf16 dispatch's per-shape kernel choice (host logic, no launch):
+    fewer tile rounds over 256 CUs, 256-row 8-phase tiles weighted 10/11 -- the
+    choices measured fastest per shape."""
+    lib = _lib.lib()
+    ph8, t320 = "gemm_bf16_8ph_kernel<256,256>", "gemm_bf16_kernel<320,256,2,4>"
+
+    def plan(M, N, K=1024):
+        return lib.aaclip_gemm_plan(_lib.BF16, M, N, K).decode()
+    # two-stream C2 pipeline: 16 images per stream
+    assert [plan(9232, n) for n in (3072, 1024, 4096)] == [ph8, ph8, t320]
+    assert plan(9232, 1024, 4096) == ph8  # c_proj
+    # whole-batch launches (bench roofline shapes)
+    assert [plan(18464, n) for n in (3072, 1024, 4096)] == [ph8, t320, ph8]
+    assert plan(577, 768) in (ph8, t320) and plan(100, 384) == "gemm_bf16_kernel<256,128,4,2>"
+    assert lib.aaclip_gemm_plan(_lib.F32, 100, 256, 64) == b"gemm_f32_kernel"
