@@ -16,7 +16,7 @@
 #include "../aa-clip_amd/csrc/attention.hip"
 
 int main(int argc, char** argv) {
-  const int B = argc > 1 ? atoi(argv[1]) : 32, N = 577, H = 16, D = H * 64, reps = 50;
+  const int B = argc > 1 ? atoi(argv[1]) : 32, N = argc > 2 ? atoi(argv[2]) : 577, H = 16, D = H * 64, reps = 50;
   const size_t nq = (size_t)B * N * 3 * D, no = (size_t)B * N * D;
   std::vector<uint16_t> h(nq);
   uint32_t x = 12345;
