@@ -28,6 +28,7 @@ from . import ops
 WIDTH = 1024
 HEADS = 16
 Q_LOG2_SCALE = 0.125 * 1.4426950408889634  # 1/sqrt(64) * log2(e)
+WS_KEEP = 8  # resident per-chunk workspaces (per image size)
 LAYERS = 24
 PATCH = 14
 EMBED = 768
@@ -132,6 +133,7 @@ class VisualEngine:
     def _workspace(self, B: int, S: int, slot: int = 0):
         key = (B, S, slot)
         if key in self._ws:
+            self._ws[key] = self._ws.pop(key)  # most recently used last
             return self._ws[key]
         g = S // PATCH
         P = g * g
@@ -166,8 +168,17 @@ class VisualEngine:
             det=e(B, EMBED, dt=torch.float32), score=e(B, dt=torch.float32),
             map=e(B, S, S, dt=torch.float32),
         )
-        # keep only the workspaces of the current (batch, size) resident
-        self._ws = {k: v for k, v in self._ws.items() if k[:2] == key[:2]}
+        # keep the workspaces of the current image size, at most WS_KEEP of them (least
+        # recently used dropped first): uneven chunks (e.g. 16 + 17 images) use one per
+        # chunk and must not evict each other. A captured graph keeps its own references
+        # (graphed_predict), so dropping an entry here never frees memory a graph replays.
+        def size_of(k):  # (B, S, slot) workspaces, ("out", B, S) chunked-output buffers
+            return k[2] if k[0] == "out" else k[1]
+
+        self._ws = {k: v for k, v in self._ws.items() if size_of(k) == S}
+        chunk_keys = [k for k in self._ws if k[0] != "out"]
+        for k in chunk_keys[:max(0, len(chunk_keys) - (WS_KEEP - 1))]:
+            del self._ws[k]
         self._ws[key] = ws
         return ws
 
@@ -277,11 +288,22 @@ class VisualEngine:
         streams > 1 splits the batch into that many image chunks, each run on its
         own HIP stream with its own workspace: the GEMM tails of one chunk
         (tile counts that leave CUs idle in the last wave) are filled by another
-        chunk's tiles. Outputs land in one [B,S,S] / [B] buffer."""
+        chunk's tiles. A tuple gives the chunk sizes explicitly (summing to B).
+        Outputs land in one [B,S,S] / [B] buffer."""
         B, S = x.shape[0], x.shape[-1]
         T = T.to(self.device, torch.float32).contiguous()
         k, s = _blur_for(domain)
-        streams = max(1, min(int(streams), B))
+        if isinstance(streams, (tuple, list)):
+            sizes = [int(v) for v in streams if int(v) > 0]
+            if sum(sizes) != B:
+                raise ValueError(f"chunk sizes {tuple(streams)} do not sum to the batch {B}")
+            bounds = [0]
+            for v in sizes:
+                bounds.append(bounds[-1] + v)
+            streams = len(sizes)
+        else:
+            streams = max(1, min(int(streams), B))
+            bounds = [(B * i) // streams for i in range(streams + 1)]
         if streams == 1:
             seg_raw, det_raw, ws = self.forward_raw(x)
             ops.anomaly_map(seg_raw, T, ws["map"], ws["grid"], g=ws["g"], ksize=k, sigma=s)
@@ -292,7 +314,6 @@ class VisualEngine:
             self._ws[key] = (torch.empty(B, S, S, device=self.device), torch.empty(B, device=self.device))
         out_map, out_score = self._ws[key]
         x = x.to(self.device, torch.float32).contiguous()
-        bounds = [(B * i) // streams for i in range(streams + 1)]
         main = torch.cuda.current_stream(self.device)
         if len(getattr(self, "_events", [])) < streams + 1:
             self._events = [torch.cuda.Event() for _ in range(streams + 1)]
@@ -330,6 +351,7 @@ class VisualEngine:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out_map, out_score = self.predict(x_s, T_s, domain, streams=streams)
+        held = list(self._ws.values())  # the workspaces the graph replays into stay allocated
 
         def run(x: torch.Tensor, T: torch.Tensor):
             x_s.copy_(x, non_blocking=True)
@@ -338,6 +360,7 @@ class VisualEngine:
             return out_map, out_score
 
         run.graph = graph
+        run.workspaces = held
         return run
 
 

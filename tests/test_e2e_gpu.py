@@ -162,7 +162,8 @@ def test_batch_composition_invariance(dev, weights, dtype):
     """Images are independent units: every per-row kernel (GEMM rows, LayerNorm rows,
     per-(image, head) attention, per-image maps/scores) computes the same bits for an
     image whatever the batch size, its position in the batch and the stream chunking
-    (size-independent property backing the B=32 bench line and the image sharding)."""
+    (size-independent property backing the B=32 bench line and the image sharding);
+    uneven explicit chunk splits and a graph captured over them included."""
     eng = _visual(weights, dtype)
     g = torch.Generator(device=dev).manual_seed(9)
     T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
@@ -173,11 +174,15 @@ def test_batch_composition_invariance(dev, weights, dtype):
         ref_m.append(m.clone())
         ref_s.append(s.clone())
     ref_m, ref_s = torch.cat(ref_m), torch.cat(ref_s)
-    for B, streams in ((7, 1), (7, 2), (7, 3), (5, 2), (3, 4)):
+    for B, streams in ((7, 1), (7, 2), (7, 3), (5, 2), (3, 4), (7, (2, 5)), (7, (4, 1, 2))):
         idx = torch.arange(7 - B, 7, device=dev) if B == 5 else torch.arange(B, device=dev)
         m, s = eng.predict(x[idx], T, "Industrial", streams=streams)
         assert torch.equal(m, ref_m[idx]), (B, streams)
         assert torch.equal(s, ref_s[idx]), (B, streams)
+    run = eng.graphed_predict(7, 336, "Industrial", streams=(3, 4))
+    eng.predict(x[:2], T, "Industrial", streams=1)  # other batch sizes in between must not disturb the graph
+    m, s = run(x, T)
+    assert torch.equal(m, ref_m) and torch.equal(s, ref_s)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
