@@ -259,6 +259,13 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     const int last_q = min(qtile * QT + QT - 1, N - 1);
     ntiles = min(ntiles, last_q / KT + 1);
   }
+  // A short key tail (non-causal, N % 64 <= 8: 577 = 9*64 + 1, 1025 = 16*64 + 1) is
+  // folded in after the tile loop as exact per-key online-softmax updates from the
+  // K/V rows in global memory, instead of a whole masked tile iteration (DMA, QK^T,
+  // softmax, P.V and a barrier for one key: 9 % of the C2 attention time).
+  const int tail_keys = causal ? 0 : N % KT;
+  const bool tail_inline = tail_keys > 0 && tail_keys <= 8;
+  if (tail_inline) ntiles = N / KT;
 
   // Ring of NS K/V stages: tile t+NS-1 is issued while tile t is computed; the
   // end-of-tile wait is COUNTED (vmcnt retires in order, 4 DMAs per wave per
@@ -306,6 +313,45 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     cur = cur + 1 == NS ? 0 : cur + 1;
   }
 #undef ATTN_WAIT_BARRIER
+  if (ntiles == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prologue's tile-0 DMA
+
+  if (tail_inline && active) {
+    const uint16_t* kt_g = base + HDt;
+    const uint16_t* vt_g = base + 2 * HDt;
+    for (int j = N - tail_keys; j < N; ++j) {
+      const uint16_t* kr = kt_g + (size_t)j * ld;
+      const uint16_t* vr = vt_g + (size_t)j * ld;
+      const bf16x8_t k0 = *(const bf16x8_t*)(kr + 8 * g), k1 = *(const bf16x8_t*)(kr + 32 + 8 * g);
+      float vv[4][4];  // V[j][d = db*16 + 4g + i], the lane's O columns
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const uint2 w = *(const uint2*)(vr + db * 16 + 4 * g);
+        vv[db][0] = bf16_to_f32((uint16_t)(w.x & 0xffff));
+        vv[db][1] = bf16_to_f32((uint16_t)(w.x >> 16));
+        vv[db][2] = bf16_to_f32((uint16_t)(w.y & 0xffff));
+        vv[db][3] = bf16_to_f32((uint16_t)(w.y >> 16));
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float sp = 0.f;  // this lane's 16 of the 64 dims (Q prescaled: log2 domain)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          sp = fmaf((float)qf[qb][0][e], (float)k0[e], fmaf((float)qf[qb][1][e], (float)k1[e], sp));
+        auto a2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(sp), __float_as_uint(sp), false, false);
+        sp = __uint_as_float(a2[0]) + __uint_as_float(a2[1]);
+        auto b2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(sp), __float_as_uint(sp), false, false);
+        sp = __uint_as_float(b2[0]) + __uint_as_float(b2[1]);
+        const float mn = fmaxf(m_run[qb], sp);
+        const float alpha = __builtin_amdgcn_exp2f(m_run[qb] - mn), p = __builtin_amdgcn_exp2f(sp - mn);
+        m_run[qb] = mn;
+        l_acc[qb][0] = fmaf(l_acc[qb][0], alpha, p);
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ot[qb][db][i] = fmaf(ot[qb][db][i], alpha, p * vv[db][i]);
+      }
+    }
+  }
 
   // ---- epilogue: O[q][d = db*16 + 4g + i] = ot / l
   if (out_mx) {

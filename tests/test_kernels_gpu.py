@@ -214,7 +214,9 @@ def _attn_ref(qkv, B, N, H, causal):
 
 
 @pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (1, 1025, 16, False),
-                                          (2, 5, 2, False), (4, 130, 4, True)])
+                                          (2, 5, 2, False), (4, 130, 4, True),
+                                          # key tails of 8 (inline per-key updates), 9 (masked tile), 0
+                                          (2, 72, 4, False), (2, 73, 4, False), (1, 64, 2, False), (3, 136, 2, False)])
 def test_attention_bf16(dev, B, N, H, causal):
     torch.manual_seed(B * N + H)
     qkv = (torch.randn(B * N, 3 * H * 64, device=dev) * 1.5).bfloat16()
