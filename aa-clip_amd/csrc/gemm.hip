@@ -910,6 +910,15 @@ int cu_count() {
   return n[dev] > 0 ? n[dev] : 256;
 }
 
+// Small M (a few images): when the big-tile choice would fill less than half of the
+// CUs, 128x128 tiles (4 waves, 2 workgroups per CU) win -- measured 1.4-2x at 1-2
+// images on every block GEMM, on out-proj / c_proj / adapters up to 8 images, and
+// never worse within 10 % where the rule picks them (tools/kbench.py --batch 1..16).
+bool prefer_small(int M, int N, bool ph8) {
+  const int64_t tiles = (int64_t)ceil_div(M, ph8 ? 256 : 320) * (N / 256);
+  return 2 * tiles < cu_count();
+}
+
 // tile rounds x tile rows, 8-phase 256-row tiles weighted 10/11 for their faster main loop
 bool prefer_8ph(int M, int N) {
   const int cus = cu_count();
@@ -940,7 +949,12 @@ extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
       break;
     default: break;
   }
-  if (N % 256 == 0 && g_gemm_variant == 0 && prefer_8ph(M, N)) return "gemm_bf16_8ph_kernel<256,256>";
+  if (N % 256 == 0 && g_gemm_variant == 0) {
+    const bool ph8 = prefer_8ph(M, N);
+    if (prefer_small(M, N, ph8)) return "gemm_bf16_kernel<128,128,2,2>";
+    if (ph8) return "gemm_bf16_8ph_kernel<256,256>";
+  }
+  if (g_gemm_variant == 9) return "gemm_bf16_kernel<128,128,2,2>";
   return N % 256 == 0 ? "gemm_bf16_kernel<320,256,2,4>" : "gemm_bf16_kernel<256,128,4,2>";
 }
 
@@ -950,7 +964,7 @@ extern "C" int aaclip_set_gemm_variant(int variant) {
   // of its 8-phase default, 8 = 320x256 everywhere); bits 4-7: tile-order
   // group height (0 = 8); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 2048 || fam > 8 || fam == 5 || fam == 7) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 2048 || fam > 9 || fam == 5 || fam == 7) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 8;
   g_setprio = (variant >> 8) & 1;
@@ -989,6 +1003,7 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
             (int64_t)N * ldw * 2 < (1ll << 31))
           return launch_bf16_8ph(a, s);
         break;
+      case 9: return launch_bf16<128, 128, 2, 2>(a, s);  // 128x128 everywhere (A/B)
       case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
         if (N % 256 == 0) return launch_bf16<320, 256, 2, 4>(a, s);
         break;
@@ -1000,9 +1015,11 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
     // pipeline (16 images per stream, M = 9232) the 8-phase kernel wins on QKV, out-proj,
     // c_proj and adapters (148-444 tiles) and the 320-row one on c_fc (464 vs 592 tiles
     // = 2 vs 3 rounds); measured per shape with tools/kbench.py, whole C2 step +5 %.
-    if (N % 256 == 0 && g_gemm_variant == 0 && (int64_t)M * lda * 2 < (1ll << 31) &&
-        (int64_t)N * ldw * 2 < (1ll << 31) && prefer_8ph(M, N))
-      return launch_bf16_8ph(a, s);
+    if (N % 256 == 0 && g_gemm_variant == 0) {
+      const bool ph8 = (int64_t)M * lda * 2 < (1ll << 31) && (int64_t)N * ldw * 2 < (1ll << 31) && prefer_8ph(M, N);
+      if (prefer_small(M, N, ph8)) return launch_bf16<128, 128, 2, 2>(a, s);
+      if (ph8) return launch_bf16_8ph(a, s);
+    }
     if (N % 256 == 0) return launch_bf16<320, 256, 2, 4>(a, s);
     return launch_bf16<256, 128, 4, 2>(a, s);
   }

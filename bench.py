@@ -99,6 +99,15 @@ def time_launches(fn, reps, stream):
     return start.elapsed_time(end) / reps  # ms per launch
 
 
+def latency_b1(eng, size, T, reps=30):
+    """Config C1's shape on the GPU: one image (bs=1) through the whole path as one
+    hipGraph replay, input already on device; HIP events on the replay stream."""
+    run = eng.graphed_predict(1, size, "Industrial", streams=1)
+    x = torch.randn(1, 3, size, size, device=T.device)
+    ms = time_launches(lambda: run(x, T), reps, torch.cuda.current_stream())
+    return {"batch": 1, "ms_per_image": round(ms, 3), "images_per_sec": round(1e3 / ms, 1)}
+
+
 def preprocess_leg(dev, batch, size, reps=20):
     """SURVEY 8(f)-3 on device: B decoded uint8 RGB images (1024x1024, MVTec's size)
     -> Pillow-exact BICUBIC resize + ToTensor + Normalize -> fp32 [B,3,S,S]
@@ -392,6 +401,7 @@ def main():
     if rank == 0 and not args.no_roofline:
         line["roofline"] = roofline_gemm(eng, ws)
         line["roofline_map"] = roofline_map(eng, ws, T)
+        line["latency_b1"] = latency_b1(eng, S, T)
     if rank == 0 and world == 1 and args.cpu_images > 0:
         line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(args.cpu_images, dev, args.streams)
     if rank == 0 and world == 1 and not args.no_roofline:

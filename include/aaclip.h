@@ -120,9 +120,10 @@ int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int
 /*
  * Tuning hook: select the bf16 GEMM tile family for benchmarking. Bits 0-3:
  * 0 = default dispatch (N % 256 == 0: per shape, 256x256 8-phase ping-pong or
- * 320x256 LDS-DMA, whichever needs fewer tile rounds weighted by per-tile cost;
- * else 256x128), 1 = 256x256 (N % 256 == 0), 2 = 256x128, 3 = 8-phase
- * everywhere, 4 = 8-phase for N >= 2048 only, 8 = 320x256 everywhere; for the
+ * 320x256 LDS-DMA, whichever needs fewer tile rounds weighted by per-tile cost,
+ * and 128x128 when that choice would fill under half the CUs; else 256x128),
+ * 1 = 256x256 (N % 256 == 0), 2 = 256x128, 3 = 8-phase everywhere, 4 = 8-phase
+ * for N >= 2048 only, 8 = 320x256 everywhere, 9 = 128x128 everywhere; for the
  * fp8 MX GEMM: 0 = 8-phase ping-pong (default), 6 = the 256x256 LDS-DMA kernel; bits 4-7:
  * tile-order group height (0 = 8); bit 8: s_setprio around the MFMA cluster;
  * bit 9: diagnostic timing mode that skips the epilogue (outputs NOT written);

@@ -74,5 +74,9 @@ def test_gemm_plan_per_shape_choice():
     assert plan(9232, 1024, 4096) == ph8  # c_proj
     # whole-batch launches (bench roofline shapes)
     assert [plan(18464, n) for n in (3072, 1024, 4096)] == [ph8, t320, ph8]
-    assert plan(577, 768) in (ph8, t320) and plan(100, 384) == "gemm_bf16_kernel<256,128,4,2>"
+    # a few images: 128x128 tiles when the big-tile choice fills under half the CUs
+    small = "gemm_bf16_kernel<128,128,2,2>"
+    assert [plan(577, n) for n in (3072, 1024, 4096)] == [small] * 3
+    assert [plan(4616, n) for n in (3072, 1024, 4096)] == [ph8, small, t320]
+    assert plan(100, 384) == "gemm_bf16_kernel<256,128,4,2>"
     assert lib.aaclip_gemm_plan(_lib.F32, 100, 256, 64) == b"gemm_f32_kernel"

@@ -31,7 +31,7 @@ def test_gemm_bf16_plain(dev, M, N, K):
     assert err < 1e-3 * ref.abs().max().item() + 1e-4, err
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 8])
+@pytest.mark.parametrize("variant", [1, 2, 3, 8, 9])
 @pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (2000, 256, 64),
                                    (18464, 3072, 1024), (577 * 40, 1024, 512), (300, 512, 128)])
 def test_gemm_bf16_variants(dev, variant, M, N, K):
@@ -108,7 +108,7 @@ def test_gemm_bf16_asymmetric_identity(dev):
     torch.testing.assert_close(out, w.float().T, atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8, 9])
 def test_gemm_epilogues_bf16(dev, variant):
     from aaclip import _lib
     _lib.call("aaclip_set_gemm_variant", variant)
