@@ -826,6 +826,13 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
 #undef PH_SYNC_MFMA
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) __builtin_amdgcn_s_barrier();
+  if (a.dbg & 1) {  // diagnostic timing path (variant bit 9): keep the MFMA results live, store nothing
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   const int mw = m0 + wr * TM, nw = n0 + wc * TN;
   const int key = a.epi;
   const int outm = a.out_dtype == AACLIP_F32 ? 0 : (a.out_dtype == AACLIP_BF16 ? 1 : 2);
@@ -1076,7 +1083,7 @@ extern "C" int aaclip_gemm_fp8mx(int out_dtype, int M, int N, int K, const void*
   AACLIP_REQUIRE(out_dtype != AACLIP_FP8 || (c_mx && ld_cmx >= M && epilogue == (AACLIP_EPI_BIAS | AACLIP_EPI_GELU)));
   if (M == 0) return AACLIP_OK;
   GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
-             out_dtype, 0, 0, 0, 0, 0, g_group_m, g_setprio, 0,
+             out_dtype, 0, 0, 0, 0, 0, g_group_m, g_setprio, g_dbg,
              nullptr, w_scale, (const uint8_t*)a_mx, ld_amx, (uint8_t*)c_mx, ld_cmx};
   // 8-phase ping-pong by default (C5 at B=32: qkv/fc/out +6-8%, c_proj +28% vs the
   // 256x256 LDS-DMA kernel; whole C5 step 1400 -> 1511 img/s); variant 6 = A/B hook
