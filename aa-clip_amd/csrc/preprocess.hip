@@ -8,14 +8,14 @@
 //     precompute_coeffs / normalize_coeffs_8bpc): per output coordinate the
 //     first source tap and the tap count, and int32 weights with 22 fraction
 //     bits (a = -0.5 cubic, support 2 * max(in/out, 1), normalised to sum 1);
-//   * kernel: two 8-bit passes, horizontal first. One workgroup owns a tile of
-//     TY output rows x 64 output columns of one image: it resamples the source
-//     rows that tile's vertical taps touch into an LDS strip of uint8 (each
-//     value clipped exactly like Pillow's intermediate image), then runs the
-//     vertical taps out of LDS and writes float32 (v / 255 - mean) / std
-//     (IEEE division, as torch's div_) into the CHW plane layout the visual
-//     embed reads. Source bytes are read once per tap through L1/L2; the
-//     strip is the only LDS traffic.
+//   * kernels: two 8-bit passes, horizontal first, each value of the
+//     intermediate clipped exactly like Pillow's intermediate image; the
+//     vertical pass writes float32 (v / 255 - mean) / std (IEEE division, as
+//     torch's div_) into the CHW plane layout the visual embed reads. Default
+//     (caller workspace): resample_h_kernel over every source row into a uint8
+//     intermediate, then resample_v_kernel. Without a workspace: one tiled
+//     kernel per (TY x TX output tile) that resamples the source rows its
+//     vertical taps touch into an LDS strip and runs the vertical taps there.
 //   * masks: nearest index tables (Pillow's accumulated xo += in/out) and a
 //     one-pass gather writing (v != 0) as float32.
 //
