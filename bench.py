@@ -201,10 +201,10 @@ def roofline_map(eng, ws, T, reps=50):
 
 def c5_leg(dev, steps: int, warmup: int, streams: int, batch: int = 32):
     """Config C5 (BASELINE.json configs[4]): 448 px (1025 tokens), 6 feature levels,
-    block GEMMs on fp8 (e4m3 weights + per-token e4m3 activations, K=128 MFMA), batch
-    of 32 on one GPU; the same workload in bf16 beside it. Accuracy of the fp8 mode:
-    its anomaly maps against the fp32 parity mode of this path (itself pinned to the
-    reference's C5 golden within 1e-5) on 2 of the images."""
+    MLP GEMMs on fp8 ("fp8": e4m3 weights + MX e4m3 activations, K=128 MFMA; QKV,
+    attention, out-proj bf16), all four block GEMMs on fp8 ("fp8_all"), and bf16,
+    batch of 32 on one GPU. Accuracy: anomaly maps against the fp32 parity mode of
+    this path (itself pinned to the reference's C5 golden within 1e-5) on 2 images."""
     S, lv = 448, (4, 8, 12, 16, 20, 24)
     vp, ad = synthetic_visual_weights(dev, seed=448, n_levels=len(lv), n_tok=(S // 14) ** 2 + 1)
     g = torch.Generator(device=dev).manual_seed(448)
@@ -213,8 +213,10 @@ def c5_leg(dev, steps: int, warmup: int, streams: int, batch: int = 32):
     out = {"workload": "C5: 448x448 (32x32 patch grid, 1025 tokens), 6 levels, batch 32, 1 GPU",
            "gflop_per_image": round(flops_per_image(1025, levels=6) / 1e9, 2)}
     maps = {}
-    for tag, dt in (("fp8", ops.FP8), ("bf16", torch.bfloat16)):
-        eng = VisualEngine(vp, ad, levels=lv, dtype=dt)
+    modes = (("fp8", dict(dtype=ops.FP8, fp8_scope="mlp")), ("fp8_all", dict(dtype=ops.FP8, fp8_scope="all")),
+             ("bf16", dict(dtype=torch.bfloat16)))
+    for tag, kw in modes:
+        eng = VisualEngine(vp, ad, levels=lv, **kw)
         run = eng.graphed_predict(batch, S, "Medical", streams=streams)
         for _ in range(warmup):
             run(x, T)
@@ -226,7 +228,7 @@ def c5_leg(dev, steps: int, warmup: int, streams: int, batch: int = 32):
         dt_s = time.perf_counter() - t0
         out[tag] = {"images_per_sec": round(batch * steps / dt_s, 2), "ms_per_step": round(dt_s / steps * 1e3, 3)}
         maps[tag] = eng.predict(x[:2], T, "Medical")[0].clone()
-        if tag == "fp8":  # the fp8 MX GEMM roofline (QKV + c_fc shapes at this size)
+        if tag == "fp8_all":  # the fp8 MX GEMM roofline (QKV + c_fc shapes at this size)
             ws = eng._workspace(batch, S)
             blk, R = eng.blocks[0], ws["x"].shape[0]
             a8, asc = ws["a8"], ws["asc"]
@@ -247,7 +249,7 @@ def c5_leg(dev, steps: int, warmup: int, streams: int, batch: int = 32):
         torch.cuda.empty_cache()
     eng = VisualEngine(vp, ad, levels=lv, dtype=torch.float32)
     ref = eng.predict(x[:2], T, "Medical")[0]
-    for tag in ("fp8", "bf16"):
+    for tag, _ in modes:
         d = maps[tag] - ref
         out[tag]["map_rel_l2_vs_fp32"] = float(d.norm() / ref.norm())
         out[tag]["map_max_abs_err_vs_fp32"] = float(d.abs().max())

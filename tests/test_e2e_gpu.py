@@ -26,10 +26,10 @@ def weights(dev):
     return t(sd), t(ia), t(ta), sd
 
 
-def _visual(weights, dtype):
+def _visual(weights, dtype, **kw):
     sd, ia, _, _ = weights
     vp = {k: v for k, v in sd.items() if k.startswith("visual.")}
-    return VisualEngine(vp, ia, dtype=dtype)
+    return VisualEngine(vp, ia, dtype=dtype, **kw)
 
 
 def _check_e2e(eng, golden, dev, map_tol):
@@ -99,8 +99,9 @@ def test_text_anchor_parity(dev, golden, weights, dtype):
             np.testing.assert_allclose(T, tx[f"{cls}_T_{key}"], atol=t_tol, rtol=t_tol * 10)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float8_e4m3fn])
-def test_c5_shapes_parity(dev, golden, dtype):
+@pytest.mark.parametrize("dtype,scope", [(torch.float32, None), (torch.bfloat16, None),
+                                         (torch.float8_e4m3fn, "mlp"), (torch.float8_e4m3fn, "all")])
+def test_c5_shapes_parity(dev, golden, dtype, scope):
     """448 px (1025 tokens), 6 levels, relu projections: map vs the reference's golden.
     float8_e4m3fn = config C5's fp8 MFMA mode (block GEMMs on e4m3 weights/activations):
     held to a documented looser bound, since e4m3 (3 mantissa bits) cannot meet the fp32
@@ -111,7 +112,8 @@ def test_c5_shapes_parity(dev, golden, dtype):
     sd = synth.clip_state_dict(111, img_size=448)
     ia, _ = synth.adapter_state_dicts(111, relu=True, n_levels=len(lv))
     vp = {k: torch.from_numpy(v).to(dev) for k, v in sd.items() if k.startswith("visual.")}
-    eng = VisualEngine(vp, {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}, levels=lv, dtype=dtype)
+    kw = dict(fp8_scope=scope) if scope else {}
+    eng = VisualEngine(vp, {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}, levels=lv, dtype=dtype, **kw)
     T = torch.from_numpy(golden["text"]["bottle_T_adapted"]).to(dev)
     x = torch.from_numpy(synth.images(111, 1, 448)).to(dev)
     maps, score = eng.predict(x, T, "Medical")
@@ -129,9 +131,9 @@ def test_c5_shapes_parity(dev, golden, dtype):
     else:
         rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
         within = np.mean(err <= 1e-3 + 1e-2 * np.abs(ref))
-        print(f"fp8 c5: map rel-L2 {rel:.3e}, frac within fp32 contract {within:.4f}, "
+        print(f"fp8 ({scope}) c5: map rel-L2 {rel:.3e}, frac within fp32 contract {within:.4f}, "
               f"score err {np.abs(score.cpu().numpy() - g['score']).max():.2e}")
-        assert rel < 0.05
+        assert rel < (0.05 if scope == "all" else 0.03)  # measured 2.5-3.8 % / 1.8 %
         np.testing.assert_allclose(score.cpu().numpy(), g["score"], atol=2e-2)
         return
     np.testing.assert_allclose(score.cpu().numpy(), g["score"], atol=1e-3)
@@ -157,14 +159,15 @@ def test_graphed_predict_matches_eager(dev, weights):
         assert torch.equal(m2, m3)
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float8_e4m3fn])
-def test_batch_composition_invariance(dev, weights, dtype):
+@pytest.mark.parametrize("dtype,scope", [(torch.bfloat16, "mlp"), (torch.float8_e4m3fn, "mlp"),
+                                         (torch.float8_e4m3fn, "all")])
+def test_batch_composition_invariance(dev, weights, dtype, scope):
     """Images are independent units: every per-row kernel (GEMM rows, LayerNorm rows,
     per-(image, head) attention, per-image maps/scores) computes the same bits for an
     image whatever the batch size, its position in the batch and the stream chunking
     (size-independent property backing the B=32 bench line and the image sharding);
     uneven explicit chunk splits and a graph captured over them included."""
-    eng = _visual(weights, dtype)
+    eng = _visual(weights, dtype, fp8_scope=scope)
     g = torch.Generator(device=dev).manual_seed(9)
     T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
     x = torch.randn(7, 3, 336, 336, device=dev, generator=g)
