@@ -54,4 +54,18 @@ __device__ __forceinline__ float wave_max(float v) {
     if (!(cond)) return AACLIP_ERR_ARG; \
   } while (0)
 
+// Dynamic-LDS opt-in for a kernel, once per device: the attribute lives in the
+// current device's context, so a process driving several GPUs sets it on each.
+// `done` is the call site's bitmask of devices already set (a race between host
+// threads only repeats the idempotent attribute write).
+inline bool lds_attr_once(const void* fn, int bytes, unsigned& done) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const unsigned bit = (dev >= 0 && dev < 32) ? 1u << dev : 0u;
+  if (bit && (done & bit)) return true;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) return false;
+  done |= bit;
+  return true;
+}
+
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }

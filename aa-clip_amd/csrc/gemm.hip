@@ -858,13 +858,8 @@ int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
   const size_t lds = 2 * 4 * 128 * 128 + 3 * 512 + 6 * 256;
-  static bool attr_set = false;  // benign race: idempotent attribute write
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)gemm_fp8mx_8ph_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
-      return AACLIP_ERR_LAUNCH;
-    attr_set = true;
-  }
+  static unsigned attr_dev = 0;
+  if (!lds_attr_once((const void*)gemm_fp8mx_8ph_kernel, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
   gemm_fp8mx_8ph_kernel<<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
@@ -875,13 +870,8 @@ int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
   const size_t lds = 2 * 4 * 128 * 128;
-  static bool attr_set = false;  // benign race: idempotent attribute write
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_8ph_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
-      return AACLIP_ERR_LAUNCH;
-    attr_set = true;
-  }
+  static unsigned attr_dev = 0;
+  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
   gemm_bf16_8ph_kernel<<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
@@ -893,13 +883,8 @@ int launch_bf16(GemmArgs a, hipStream_t s) {
   a.tiles_m = ceil_div(a.M, BM);
   a.tiles_n = a.N / BN;
   const size_t lds = 2 * (size_t)(BM + BN) * 128 + (Q == 2 ? 2 * BM * 2 : 0);
-  static bool attr_set = false;  // benign race: idempotent attribute write
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, Q>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return AACLIP_ERR_LAUNCH;
-    attr_set = true;
-  }
+  static unsigned attr_dev = 0;
+  if (!lds_attr_once((const void*)gemm_bf16_kernel<BM, BN, WM, WN, Q>, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
   gemm_bf16_kernel<BM, BN, WM, WN, Q><<<a.tiles_m * a.tiles_n, WM * WN * 64, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;

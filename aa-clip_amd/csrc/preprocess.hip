@@ -429,15 +429,10 @@ extern "C" int aaclip_preprocess_images(const uint8_t* src, int64_t img_stride, 
   if (workspace && workspace_bytes >= (size_t)batch * in_h * tstride && hlds && kx <= HK && out_size <= 1024 &&
       batch <= 65535 &&
       !getenv("AACLIP_PREP_TILE")) {
-    static bool h_attr = false;  // benign race: idempotent attribute writes
-    if (!h_attr) {
-      if (hipFuncSetAttribute((const void*)resample_h_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              H_LDS) != hipSuccess ||
-          hipFuncSetAttribute((const void*)resample_h_kernel<HK>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              H_LDS) != hipSuccess)
-        return AACLIP_ERR_LAUNCH;
-      h_attr = true;
-    }
+    static unsigned h8_dev = 0, hk_dev = 0;
+    if (!lds_attr_once((const void*)resample_h_kernel<8>, H_LDS, h8_dev) ||
+        !lds_attr_once((const void*)resample_h_kernel<HK>, H_LDS, hk_dev))
+      return AACLIP_ERR_LAUNCH;
     HArgs h{src, img_stride, row_pitch, in_h, in_w, out_size, hrows, x_bounds, x_coeffs, kx, srow, tstride,
             (uint8_t*)workspace};
     const dim3 hgrid(ceil_div(in_h, hrows), batch);
@@ -486,15 +481,10 @@ extern "C" int aaclip_preprocess_images(const uint8_t* src, int64_t img_stride, 
   a.tiles_x = ceil_div(out_size, a.tx);
   a.tiles_y = ceil_div(out_size, a.ty);
   AACLIP_REQUIRE(batch <= 65535 && (int64_t)a.tiles_x * a.tiles_y < (1ll << 31));
-  static bool attr_set = false;  // benign race: idempotent attribute writes
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)bicubic_normalize_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            STAGED_LDS) != hipSuccess ||
-        hipFuncSetAttribute((const void*)bicubic_normalize_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            DIRECT_LDS) != hipSuccess)
-      return AACLIP_ERR_LAUNCH;
-    attr_set = true;
-  }
+  static unsigned staged_dev = 0, direct_dev = 0;
+  if (!lds_attr_once((const void*)bicubic_normalize_kernel<true>, STAGED_LDS, staged_dev) ||
+      !lds_attr_once((const void*)bicubic_normalize_kernel<false>, DIRECT_LDS, direct_dev))
+    return AACLIP_ERR_LAUNCH;
   const dim3 grid(a.tiles_x * a.tiles_y, batch);
   if (staged)
     bicubic_normalize_kernel<true><<<grid, NT, lds, (hipStream_t)stream>>>(a);
