@@ -180,6 +180,10 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
                                                         int64_t ld_mx) {
   const int causal = flags & AACLIP_ATTN_CAUSAL;
   constexpr int NS = ATTN_STAGES;
+  // the prologue fills NS-1 <= 2 stages and the counted waits assume <= 2 tiles in
+  // flight: a 4-stage ring would read a never-filled slot (measured: checksums
+  // differ run to run), so only 2 and 3 are valid
+  static_assert(NS == 2 || NS == 3, "ATTN_STAGES must be 2 or 3");
   __shared__ __attribute__((aligned(16))) char smem[NS * 2 * KT * 128];  // [stage][K|V][64][128B]
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
