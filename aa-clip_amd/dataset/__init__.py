@@ -120,10 +120,14 @@ def collate_raw(items):
 
 def get_dataset(dataset_name: str, img_size: int, training_mode: str, shot: int = -1, stage: str = "train",
                 logger=None, synthetic_n: int = 16, raw: bool = False):
-    if dataset_name == "synthetic":
+    if dataset_name in ("synthetic", "synthetic_mvtec"):
         if stage not in ("test", "visualize"):
             raise ValueError("the synthetic dataset only has a test stage")
-        return {"bottle": SyntheticSingleClassDataset(synthetic_n, img_size)}
+        if dataset_name == "synthetic":
+            return {"bottle": SyntheticSingleClassDataset(synthetic_n, img_size)}
+        # config C4's shape: every MVTec class, its own seed
+        return {c: SyntheticSingleClassDataset(synthetic_n, img_size, class_name=c, seed=111 + i)
+                for i, c in enumerate(CLASS_NAMES["synthetic_mvtec"])}
     if "Med" not in dataset_name:
         assert dataset_name in DATA_PATH, (
             f"Dataset {dataset_name} not found; available datasets: {list(DATA_PATH.keys())}")

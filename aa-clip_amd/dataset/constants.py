@@ -18,3 +18,8 @@ PROMPTS = _T["PROMPTS"]
 CLASS_NAMES["synthetic"] = ["bottle"]
 REAL_NAMES["synthetic"] = {"bottle": REAL_NAMES["MVTec"]["bottle"]}
 DOMAINS["synthetic"] = "Industrial"
+# Build-only entry: config C4's flow (MVTec-AD's 15 classes and their ensemble
+# prompts, Industrial blur) on seeded synthetic images and masks.
+CLASS_NAMES["synthetic_mvtec"] = list(CLASS_NAMES["MVTec"])
+REAL_NAMES["synthetic_mvtec"] = dict(REAL_NAMES["MVTec"])
+DOMAINS["synthetic_mvtec"] = "Industrial"

@@ -92,9 +92,11 @@ class AdaptedCLIP(nn.Module):
         """(list[len(levels)] of [B, P, 768] unit-norm patch features, det [B, 768])."""
         return self.visual_engine().forward(x)
 
-    def predict(self, x, text_features, domain="Industrial"):
-        """Fused test path (test.py:80-93): (anomaly map [B,S,S], image score [B]), fp32."""
-        return self.visual_engine().predict(x, text_features, domain)
+    def predict(self, x, text_features, domain="Industrial", streams=1):
+        """Fused test path (test.py:80-93): (anomaly map [B,S,S], image score [B]), fp32.
+        streams > 1 (or a tuple of chunk sizes) runs image chunks on that many HIP
+        streams (VisualEngine.predict); per-image results do not depend on it."""
+        return self.visual_engine().predict(x, text_features, domain, streams=streams)
 
     def encode_text(self, text, adapt_text=True):
         if not adapt_text:

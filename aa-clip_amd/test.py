@@ -3,6 +3,7 @@ same flow, same outputs), running AdaptedCLIP on the MI355X kernels.
 
     python test.py --dataset MVTec --img_size 336 --save_path ckpt/...     (needs weights + data)
     python test.py --dataset synthetic --allow_random_init --img_size 336  (C1: no files needed)
+    python test.py --dataset synthetic_mvtec --allow_random_init --img_size 336  (C4's 15-class flow)
 
 Differences from the reference, all on the host side:
   * the per-batch loop calls the fused AdaptedCLIP.predict (map + score in one
@@ -130,7 +131,8 @@ def main(argv=None):
         logger.info("-----------------------------------------------")
         logger.info("load model from epoch %d", test_epoch)
         logger.info("-----------------------------------------------")
-        raw = args.gpu_preprocess and args.dataset != "synthetic"  # synthetic items are already normalised
+        synthetic = args.dataset.startswith("synthetic")
+        raw = args.gpu_preprocess and not synthetic  # synthetic items are already normalised
         image_datasets = get_dataset(args.dataset, args.img_size, None, args.shot, "test", logger=logger,
                                      synthetic_n=args.synthetic_n, raw=raw)
         prep = None
@@ -141,7 +143,7 @@ def main(argv=None):
             text_embeddings = get_adapted_text_embedding(model if adapt_text else clip_model, args.dataset, device)
         df = DataFrame(columns=["class name", "pixel AUC", "pixel AP", "image AUC", "image AP"])
         for class_name, image_dataset in image_datasets.items():
-            workers = 0 if args.dataset == "synthetic" else 4
+            workers = 0 if synthetic else 4
             from dataset import collate_raw
             loader = torch.utils.data.DataLoader(image_dataset, batch_size=args.batch_size, shuffle=False,
                                                  num_workers=workers, pin_memory=True,

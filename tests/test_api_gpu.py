@@ -74,3 +74,14 @@ def test_harness_synthetic_c1(tmp_path):
                        "--synthetic_n", "16", "--save_path", str(tmp_path)])
     row = df.iloc[0]
     assert 0.0 <= row["pixel AUC"] <= 100.0 and 0.0 <= row["image AUC"] <= 100.0
+
+
+def test_harness_synthetic_mvtec_c4(tmp_path):
+    """Config C4's flow (15 MVTec classes, each with its ensemble prompts, per-class
+    metrics + the Average row) on synthetic images through the test.py counterpart."""
+    import test as harness
+    df = harness.main(["--dataset", "synthetic_mvtec", "--allow_random_init", "--img_size", "336",
+                       "--batch_size", "2", "--synthetic_n", "2", "--save_path", str(tmp_path)])
+    assert len(df) == 16 and df.iloc[-1]["class name"] == "Average"
+    for _, row in df.iterrows():
+        assert 0.0 <= row["pixel AUC"] <= 100.0 and 0.0 <= row["image AUC"] <= 100.0

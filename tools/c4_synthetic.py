@@ -1,0 +1,156 @@
+"""Config C4 on synthetic data (GPU): the MVTec-AD eval flow — 15 classes, each
+class's ensemble prompts through the adapted text tower, per-class batches of
+images through forward + 4-level map + image score, per-class metrics_eval
+(pixel/image AUROC + AP) — on the drop-in API (model.adapter / forward_utils,
+test.py:185-236), with synthetic weights (oracle/synth.py) and seeded synthetic
+images/masks (dataset "synthetic_mvtec"). MVTec images and the OpenAI/AA-CLIP
+checkpoints are absent here, so the absolute AUROCs mean nothing; what this
+measures is the whole-eval rate and the parity of every per-class metric with
+the CPU reference (numpy oracle + sklearn) on the same inputs.
+
+usage: python tools/c4_synthetic.py [--n 32] [--cpu-n 2] [--out FILE]
+  --n      images per class on the GPU (timed flow, bf16)
+  --cpu-n  images per class in the parity subset (first cpu-n of each class:
+           normal + anomalous), run through the oracle and through the GPU in
+           fp32 and bf16; metrics compared per class
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "aa-clip_amd")]
+from dataset import DOMAINS, get_dataset  # noqa: E402
+from forward_utils import _sentences, get_adapted_text_embedding, metrics_eval  # noqa: E402
+from model.adapter import AdaptedCLIP  # noqa: E402
+from model.clip import create_model  # noqa: E402
+from model.tokenizer import tokenize  # noqa: E402
+from dataset.constants import REAL_NAMES  # noqa: E402
+from oracle import aaclip_np as R  # noqa: E402
+from oracle import synth  # noqa: E402
+
+DS = "synthetic_mvtec"
+
+
+def build(dev, dtype):
+    clip = create_model("ViT-L-14-336", 336, pretrained=None, device=dev)
+    clip.load_state_dict({k: torch.from_numpy(v) for k, v in synth.clip_state_dict(111).items()}, strict=True)
+    m = AdaptedCLIP(clip, relu=False, compute_dtype=dtype).to(dev).eval()
+    ia, ta = synth.adapter_state_dicts(111)
+    m.image_adapter.load_state_dict({k: torch.from_numpy(v) for k, v in ia.items()})
+    m.text_adapter.load_state_dict({k: torch.from_numpy(v) for k, v in ta.items()})
+    return m
+
+
+def class_batches(ds, n, bs):
+    for b0 in range(0, n, bs):
+        items = [ds[i] for i in range(b0, min(n, b0 + bs))]
+        yield (torch.stack([it["image"] for it in items]), np.stack([it["mask"].numpy() for it in items]),
+               np.array([it["label"] for it in items]))
+
+
+def gpu_eval(model, datasets, n, bs, dev, pinned):
+    """test.py:185-236 for every class; returns per-class metrics, maps, scores."""
+    dom = DOMAINS[DS]
+    out = {}
+    with torch.no_grad():
+        T = get_adapted_text_embedding(model, DS, dev)
+        for c, ds in datasets.items():
+            masks, labels, preds, scores = [], [], [], []
+            for img, msk, lab in pinned[c] if pinned else class_batches(ds, n, bs):
+                pmap, s = model.predict(img.to(dev, non_blocking=True), T[c], dom, streams=2)
+                preds.append(pmap.clone())
+                scores.append(s.clone())
+                masks.append(msk)
+                labels.append(lab)
+            masks, labels = np.concatenate(masks), np.concatenate(labels)
+            preds, scores = torch.cat(preds), torch.cat(scores)
+            out[c] = (metrics_eval(masks, labels, preds, scores, c, domain=dom), preds, scores, masks, labels)
+    return T, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=32)
+    ap.add_argument("--cpu-n", type=int, default=2)
+    ap.add_argument("--bs", type=int, default=32)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    datasets = get_dataset(DS, 336, None, -1, "test", synthetic_n=a.n)
+    # host-side batches prepared once (pinned), as the DataLoader workers would
+    pinned = {c: [(img.pin_memory(), m, lab) for img, m, lab in class_batches(ds, a.n, a.bs)]
+              for c, ds in datasets.items()}
+    res = {"workload": f"C4-synthetic: 15 MVTec classes x {a.n} synthetic 336px images, ensemble prompts "
+                       f"(adapted text tower), batch {a.bs}, 4 levels, metrics_eval per class, 1 GPU",
+           "data": "synthetic weights (oracle/synth.py) and seeded synthetic images/masks (dataset synthetic_mvtec)"}
+    model = build(dev, torch.bfloat16)
+    gpu_eval(model, datasets, a.n, a.bs, dev, pinned)  # warm-up: engines, workspaces, graphs
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, out16 = gpu_eval(model, datasets, a.n, a.bs, dev, pinned)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n_img = a.n * len(datasets)
+    res["bf16_whole_eval"] = {"seconds": round(dt, 4), "images": n_img, "images_per_sec": round(n_img / dt, 1),
+                              "includes": "H2D copies of the pinned batches, 15 text anchors (240 prompts), "
+                                          "forward + map + score, per-class device metrics"}
+    mean = {k: float(np.mean([out16[c][0][k] for c in out16])) for k in ("pixel AUC", "pixel AP", "image AUC",
+                                                                        "image AP")}
+    res["bf16_mean_metrics"] = mean
+    del model
+    torch.cuda.empty_cache()
+
+    # parity subset: first cpu-n images of each class through the oracle and the GPU (fp32, bf16)
+    if a.cpu_n > 0:
+        sd = synth.clip_state_dict(111)
+        ia, ta = synth.adapter_state_dicts(111)
+        par = {}
+        t0 = time.perf_counter()
+        ref = {}
+        for c, ds in datasets.items():
+            sn, sa = _sentences(REAL_NAMES[DS][c])
+            Tc = R.class_anchor(sd, ta, tokenize(sn).numpy(), tokenize(sa).numpy())
+            img, msk, lab = next(class_batches(ds, a.cpu_n, a.cpu_n))
+            seg, det = R.visual_forward(sd, ia, img.numpy())
+            maps = R.anomaly_map(seg, Tc, 336, DOMAINS[DS])
+            sc = R.image_score(det, Tc)
+            ref[c] = (Tc, R.metrics_eval(msk[:, 0], lab, maps, sc, c, DOMAINS[DS]), maps, sc)
+        cpu_dt = time.perf_counter() - t0
+        for tag, dt_ in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+            model = build(dev, dt_)
+            sub = {c: [tuple(next(class_batches(ds, a.cpu_n, a.cpu_n)))] for c, ds in datasets.items()}
+            T, out = gpu_eval(model, datasets, a.cpu_n, a.cpu_n, dev, sub)
+            rows = {}
+            for c in datasets:
+                g, r = out[c][0], ref[c][1]
+                rows[c] = {k: round(abs(float(g[k]) - float(r[k])), 4) for k in ("pixel AUC", "pixel AP",
+                                                                                  "image AUC", "image AP")}
+                rows[c]["anchor_max_abs_err"] = float(np.abs(T[c].cpu().numpy() - ref[c][0]).max())
+                m = out[c][1].cpu().numpy()
+                rows[c]["map_max_abs_err"] = float(np.abs(m - ref[c][2]).max())
+                rows[c]["map_frac_within_tol"] = float((np.abs(m - ref[c][2]) <= 1e-3 + 1e-2 * np.abs(ref[c][2])).mean())
+            par[tag] = {"max_metric_abs_diff_pct_points": max(max(v[k] for k in ("pixel AUC", "pixel AP", "image AUC",
+                                                                                 "image AP")) for v in rows.values()),
+                        "max_anchor_abs_err": max(v["anchor_max_abs_err"] for v in rows.values()),
+                        "max_map_abs_err": max(v["map_max_abs_err"] for v in rows.values()),
+                        "min_map_frac_within_tol": min(v["map_frac_within_tol"] for v in rows.values()),
+                        "per_class": rows}
+            del model
+            torch.cuda.empty_cache()
+        res["parity"] = {"images_per_class": a.cpu_n, "reference": "numpy oracle + sklearn (CPU), same weights/inputs",
+                         "cpu_seconds": round(cpu_dt, 1), **par}
+    line = json.dumps(res)
+    print(line, flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
