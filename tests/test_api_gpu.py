@@ -85,3 +85,13 @@ def test_harness_synthetic_mvtec_c4(tmp_path):
     assert len(df) == 16 and df.iloc[-1]["class name"] == "Average"
     for _, row in df.iterrows():
         assert 0.0 <= row["pixel AUC"] <= 100.0 and 0.0 <= row["image AUC"] <= 100.0
+
+
+def test_batched_text_anchors_equal_per_class(dev, model):
+    """get_adapted_text_embedding encodes every prompt of the dataset in one call:
+    each class's anchors must equal the per-class path bit for bit."""
+    from forward_utils import get_adapted_single_class_text_embedding, get_adapted_text_embedding
+    with torch.no_grad():
+        allT = get_adapted_text_embedding(model, "MVTec", dev)
+        for c in ("bottle", "screw", "zipper"):
+            assert torch.equal(allT[c], get_adapted_single_class_text_embedding(model, "MVTec", c, dev)), c
