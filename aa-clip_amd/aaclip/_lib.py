@@ -15,6 +15,7 @@ ABI_VERSION = 2
 F32 = 0
 BF16 = 1
 FP8 = 2
+F16 = 3
 EPI_BIAS = 1
 EPI_GELU = 2
 EPI_LEAKY = 4

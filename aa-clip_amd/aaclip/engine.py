@@ -60,7 +60,10 @@ def _quant_weight_fp8(w: torch.Tensor):
 class VisualEngine:
     def __init__(self, vparams: dict, adapter: dict, *, levels=(6, 12, 18, 24), image_adapt_until=6,
                  image_adapt_weight=0.1, dtype=torch.bfloat16, fold_q_scale=True, fp8_scope="mlp"):
-        """dtype: bfloat16 (perf path), float32 (parity mode) or float8_e4m3fn (config C5:
+        """dtype: bfloat16 (perf path), float16 (parity-grade 16-bit path: fp16 MFMA at the
+        bf16 rate with 8x finer operand rounding; the weights the OpenAI loader produces
+        are fp16-exact, reference model/model.py:366), float32 (fp32-MFMA parity mode) or
+        float8_e4m3fn (config C5:
         block GEMMs on e4m3 weights (per-output-channel scales) and MX e4m3 activations
         (e8m0 scale per 64 values, applied by the K=128 block-scaled MFMA), every input
         written in that format by its producer (LayerNorm / attention / c_fc epilogues).
@@ -68,8 +71,8 @@ class VisualEngine:
         bf16 -- measured at C5: map rel-L2 0.9 % vs the fp32 mode at +24 % images/s over
         bf16; "all" = the four block GEMMs in fp8: +38 % but 8 % map rel-L2 (e4m3 q/k
         logits amplified by the softmax)."""
-        if dtype not in (torch.bfloat16, torch.float32, FP8):
-            raise ValueError("dtype must be bfloat16, float32 or float8_e4m3fn")
+        if dtype not in (torch.bfloat16, torch.float16, torch.float32, FP8):
+            raise ValueError("dtype must be bfloat16, float16, float32 or float8_e4m3fn")
         self.fp8 = dtype == FP8
         if fp8_scope not in ("all", "mlp"):
             raise ValueError("fp8_scope must be 'all' (QKV, out-proj, c_fc, c_proj) or 'mlp' (c_fc, c_proj)")
@@ -156,7 +159,7 @@ class VisualEngine:
             g=g, P=P, n_tok=n_tok,
             cols=e(B * P, KPATCH), x=e(R, WIDTH, dt=torch.float32), h=e(R, WIDTH), qkv=e(R, 3 * WIDTH),
             attn=e(R, WIDTH), fc=e(R, 4 * WIDTH), u=e(R, WIDTH, dt=torch.float32),
-            xb=e(R, WIDTH, dt=torch.bfloat16) if cdt == torch.bfloat16 else None,
+            xb=e(R, WIDTH) if cdt != torch.float32 else None,  # 16-bit adapter input (bf16 / fp16)
             taps=[e(B * P, WIDTH) for _ in range(L)],
             # all level projections + det in one [B*P, (L+1)*768] fp32 buffer: level l at
             # columns l*768, det_proj at L*768 (one row stride for the map kernel).
@@ -428,7 +431,7 @@ class TextEngine:
         e = lambda *s, dt=cdt: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
         X, H = e(R, W, dt=torch.float32), e(R, W)
         qkv, att, fc, u = e(R, 3 * W), e(R, W), e(R, 4 * W), e(R, W, dt=torch.float32)
-        xb = e(R, W, dt=torch.bfloat16) if cdt == torch.bfloat16 else None
+        xb = e(R, W) if cdt != torch.float32 else None
         ops.text_embed_ln(tokens, self.tok_emb, self.pos, self.blocks[0]["ln1"], X, H)
         nb = len(self.blocks)
         for i, blk in enumerate(self.blocks):

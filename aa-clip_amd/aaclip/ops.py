@@ -12,20 +12,20 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import BF16, F32, call
+from ._lib import BF16, F16, F32, call
 
-_DT = {torch.float32: F32, torch.bfloat16: BF16}
+_DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16}
 
 
 def dtag(t: torch.Tensor) -> int:
     try:
         return _DT[t.dtype]
     except KeyError:
-        raise TypeError(f"unsupported dtype {t.dtype}; expected float32 or bfloat16") from None
+        raise TypeError(f"unsupported dtype {t.dtype}; expected float32, bfloat16 or float16") from None
 
 
 def torch_dtype(tag: int) -> torch.dtype:
-    return torch.float32 if tag == F32 else torch.bfloat16
+    return {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}[tag]
 
 
 def _stream() -> int:
@@ -56,6 +56,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
         _rowmajor(t, n)
     if a.dtype != w.dtype:
         raise TypeError("gemm operands must share a dtype")
+    if out.dtype not in (torch.float32, a.dtype) and not (a.dtype == torch.float32 and out.dtype == torch.bfloat16):
+        raise TypeError("gemm output must be float32 or the operands' 16-bit dtype")
     M, K = a.shape
     N = w.shape[0]
     if w.shape[1] != K or out.shape[1] != N:
@@ -63,7 +65,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
     rows_out = M if row_group == 0 else ((M - 1) // row_group) * row_group_out + row_offset + (M - 1) % row_group + 1
     if out.shape[0] < rows_out or (row_group and M % row_group):
         raise ValueError("gemm output rows too small for the row remap")
-    epi, ldr, ldaux = _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux)
+    epi, ldr, ldaux = _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux,
+                                      aux_dtype=torch.float16 if a.dtype == torch.float16 else torch.bfloat16)
     call("aaclip_gemm", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w), w.stride(0),
          _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
          row_group, row_group_out, row_offset, _stream())
@@ -162,7 +165,7 @@ def gemm_fp8mx(a: torch.Tensor, a_sc: torch.Tensor, w: torch.Tensor, w_scale: to
     return out
 
 
-def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux):
+def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux, aux_dtype=torch.bfloat16):
     epi = 0
     if bias is not None:
         if bias.dtype != torch.float32 or bias.numel() != N:
@@ -182,8 +185,8 @@ def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux):
     ldaux = 0
     if aux is not None:
         _rowmajor(aux, "aux")
-        if aux.dtype != torch.bfloat16 or aux.shape[1] != N or aux.shape[0] < rows_out:
-            raise ValueError("aux must be bf16 [rows, N]")
+        if aux.dtype != aux_dtype or aux.shape[1] != N or aux.shape[0] < rows_out:
+            raise ValueError(f"aux must be {aux_dtype} [rows, N] (fp16 for fp16 operands, else bf16)")
         epi |= _lib.EPI_AUX_BF16
         ldaux = aux.stride(0)
     return epi, ldr, ldaux
@@ -193,11 +196,11 @@ def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux):
 def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int,
               causal: bool = False, out_sc=None, q_prescaled: bool = False) -> torch.Tensor:
     """out = MHA core of packed qkv; out fp8 (e4m3) + out_sc = MX output (bf16 qkv only).
-    q_prescaled: the q columns already carry log2(e)/sqrt(64) (bf16 qkv only)."""
+    q_prescaled: the q columns already carry log2(e)/sqrt(64) (bf16 / fp16 qkv only)."""
     _dev(qkv, out, out_sc)
     flags = (_lib.ATTN_CAUSAL if causal else 0) | (_lib.ATTN_Q_PRESCALED if q_prescaled else 0)
-    if q_prescaled and qkv.dtype != torch.bfloat16:
-        raise ValueError("q_prescaled needs bf16 qkv")
+    if q_prescaled and qkv.dtype not in (torch.bfloat16, torch.float16):
+        raise ValueError("q_prescaled needs bf16 or fp16 qkv")
     hd = 64
     if qkv.shape != (batch * seq, 3 * heads * hd) or out.shape != (batch * seq, heads * hd):
         raise ValueError("attention shape mismatch")

@@ -25,13 +25,30 @@ def gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     """All-gather variable-size row shards (produced by shard_range order) into the
     global [n_total, ...] tensor on every rank. One collective: shards are padded
     to the largest shard, gathered with all_gather_into_tensor, then trimmed."""
-    world = dist.get_world_size(group)
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     if world == 1:
         return local
     sizes = [shard_range(n_total, r, world) for r in range(world)]
     width = max(b - a for a, b in sizes)
+    if width * world == n_total:  # even shards (e.g. C3: 256 = 8 x 32): gather in place, no pad/trim
+        out = torch.empty((n_total,) + tuple(local.shape[1:]), device=local.device, dtype=local.dtype)
+        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+        return out
     pad = torch.zeros((width,) + tuple(local.shape[1:]), device=local.device, dtype=local.dtype)
     pad[: local.shape[0]] = local
     out = torch.empty((world * width,) + tuple(local.shape[1:]), device=local.device, dtype=local.dtype)
     dist.all_gather_into_tensor(out, pad, group=group)
     return torch.cat([out[r * width: r * width + (b - a)] for r, (a, b) in enumerate(sizes)], 0)
+
+
+def sharded_step(predict, x_local: torch.Tensor, T: torch.Tensor, n_total: int, group=None,
+                 gather_maps: bool = False):
+    """One data-parallel step of the path: this rank's shard of the global batch
+    (shard_range order) through `predict(x, T) -> (maps [b, ...], scores [b])`, then
+    the path's only exchange, the all-gather of the per-image scores (and of the
+    maps when the caller needs them, e.g. for metrics_eval on rank 0).
+    Returns (local maps, local scores, global scores [n_total], global maps or None)."""
+    maps, scores = predict(x_local, T)
+    s_all = gather_rows(scores, n_total, group)
+    m_all = gather_rows(maps, n_total, group) if gather_maps else None
+    return maps, scores, s_all, m_all

@@ -63,10 +63,12 @@ __device__ __forceinline__ float max_over_groups(float v) {
 // bf16-rounded p.
 constexpr float kRescaleLog2 = 8.0f;
 
-template <int NKB, int NQB, bool MASK>
-__device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&qf)[2][2], float4_t (&ot)[2][4],
+template <int NKB, int NQB, bool MASK, bool H16>
+__device__ __forceinline__ void attn_tile(const char* kt_lds, const h16x8_t<H16> (&qf)[2][2], float4_t (&ot)[2][4],
                                           float (&m_run)[2], float4_t (&l_acc)[2], int key0, int q0, int N,
                                           int causal, int g, int c, bool first) {
+  using V8 = h16x8_t<H16>;
+  using E = h16_t<H16>;
   const char* vt_lds = kt_lds + KT * 128;
   float4_t st[NQB][NKB];
 #pragma unroll
@@ -79,14 +81,13 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
   for (int kb = 0; kb < NKB; ++kb) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t kf = *(const bf16x8_t*)(kt_lds + swz(kb * 16 + c, ks * 4 + g));
+      const V8 kf = *(const V8*)(kt_lds + swz(kb * 16 + c, ks * 4 + g));
 #pragma unroll
-      for (int qb = 0; qb < NQB; ++qb)
-        st[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qb][ks], st[qb][kb], 0, 0, 0);
+      for (int qb = 0; qb < NQB; ++qb) st[qb][kb] = mfma16(kf, qf[qb][ks], st[qb][kb]);
     }
   }
   constexpr int NKS = (NKB + 1) / 2;  // 32-key MFMA steps for P.V
-  bf16x8_t pf[NQB][NKS];
+  V8 pf[NQB][NKS];
 #pragma unroll
   for (int qb = 0; qb < NQB; ++qb) {
     float mx = -INFINITY;
@@ -131,23 +132,21 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
       for (int i = 0; i < 4; ++i) p[kb][i] = kb < NKB ? __builtin_amdgcn_exp2f(st[qb][kb < NKB ? kb : 0][i]) : 0.f;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      bf16x8_t v;
+      V8 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        v[i] = (__bf16)p[2 * ks][i];
-        v[4 + i] = (__bf16)p[2 * ks + 1][i];
+        v[i] = (E)p[2 * ks][i];
+        v[4 + i] = (E)p[2 * ks + 1][i];
       }
       pf[qb][ks] = v;
     }
   }
   // l += 1 . P^T
-  const bf16x8_t ones = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
-                         (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
+  const V8 ones = {(E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f};
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-    for (int qb = 0; qb < NQB; ++qb)
-      l_acc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qb][ks], l_acc[qb], 0, 0, 0);
+    for (int qb = 0; qb < NQB; ++qb) l_acc[qb] = mfma16(ones, pf[qb][ks], l_acc[qb]);
   // O^T += V^T . P^T ; V^T fragment via transposing LDS reads
 #pragma unroll
   for (int db = 0; db < 4; ++db) {
@@ -159,10 +158,9 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
       const short4_t lo = tr_read(vt_lds + swz(r0, chunk) + (pp & 1) * 8);
       const short4_t hi = tr_read(vt_lds + swz(r0 + 16, chunk) + (pp & 1) * 8);
       const short8_t vv = short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, vv);
+      const V8 vf = __builtin_bit_cast(V8, vv);
 #pragma unroll
-      for (int qb = 0; qb < NQB; ++qb)
-        ot[qb][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb][ks], ot[qb][db], 0, 0, 0);
+      for (int qb = 0; qb < NQB; ++qb) ot[qb][db] = mfma16(vf, pf[qb][ks], ot[qb][db]);
     }
   }
 }
@@ -174,6 +172,8 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const bf16x8_t (&q
 #define ATTN_OCC 3  // workgroups per CU the register budget is sized for
 #endif
 
+// H16: fp16 q/k/v/p on v_mfma_f32_16x16x32_f16 (the parity-grade mode), else bf16.
+template <bool H16>
 __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
                                                         uint16_t* __restrict__ out, int batch, int N, int H,
                                                         int flags, uint8_t* __restrict__ out_mx,
@@ -184,6 +184,8 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   // flight: a 4-stage ring would read a never-filled slot (measured: checksums
   // differ run to run), so only 2 and 3 are valid
   static_assert(NS == 2 || NS == 3, "ATTN_STAGES must be 2 or 3");
+  using V8 = h16x8_t<H16>;
+  using E = h16_t<H16>;
   __shared__ __attribute__((aligned(16))) char smem[NS * 2 * KT * 128];  // [stage][K|V][64][128B]
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -205,12 +207,12 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   const int q0 = qtile * QT + wid * QW;
 
   // ---- Q fragments (B operand of K.Q^T): lane holds Q[q][ks*32 + 8g .. +7]
-  bf16x8_t qf[2][2];
+  V8 qf[2][2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const int q = min(q0 + qb * 16 + c, N - 1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[qb][ks] = *(const bf16x8_t*)(base + (size_t)q * ld + ks * 32 + 8 * g);
+    for (int ks = 0; ks < 2; ++ks) qf[qb][ks] = *(const V8*)(base + (size_t)q * ld + ks * 32 + 8 * g);
   }
   if (!(flags & AACLIP_ATTN_Q_PRESCALED)) {  // log2(e)/sqrt(64) not folded by the caller: apply it here
     constexpr float sl2 = 0.125f * 1.4426950408889634f;
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (__bf16)((float)qf[qb][ks][e] * sl2);
+        for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (E)((float)qf[qb][ks][e] * sl2);
   }
 
   // ---- DMA sources: wave w loads pieces i*4+w (8 rows each) of the K and V tiles
@@ -297,7 +299,7 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   for (; t < nfull; ++t) {
     const bool deep = advance();
     if (active)
-      attn_tile<4, 2, false>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g, c,
+      attn_tile<4, 2, false, H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g, c,
                              t == 0);
     if (deep) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
     cur = cur + 1 == NS ? 0 : cur + 1;
@@ -309,9 +311,9 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     const int live = min(KT, N - key0);  // valid keys in this tile
     if (active) {
       const bool first = t == 0;
-      if (live > 32) attn_tile<4, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
-      else if (live > 16) attn_tile<2, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
-      else attn_tile<1, 2, true>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
+      if (live > 32) attn_tile<4, 2, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
+      else if (live > 16) attn_tile<2, 2, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
+      else attn_tile<1, 2, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
     }
     if (deep) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
     cur = cur + 1 == NS ? 0 : cur + 1;
@@ -325,15 +327,15 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     for (int j = N - tail_keys; j < N; ++j) {
       const uint16_t* kr = kt_g + (size_t)j * ld;
       const uint16_t* vr = vt_g + (size_t)j * ld;
-      const bf16x8_t k0 = *(const bf16x8_t*)(kr + 8 * g), k1 = *(const bf16x8_t*)(kr + 32 + 8 * g);
+      const V8 k0 = *(const V8*)(kr + 8 * g), k1 = *(const V8*)(kr + 32 + 8 * g);
       float vv[4][4];  // V[j][d = db*16 + 4g + i], the lane's O columns
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
         const uint2 w = *(const uint2*)(vr + db * 16 + 4 * g);
-        vv[db][0] = bf16_to_f32((uint16_t)(w.x & 0xffff));
-        vv[db][1] = bf16_to_f32((uint16_t)(w.x >> 16));
-        vv[db][2] = bf16_to_f32((uint16_t)(w.y & 0xffff));
-        vv[db][3] = bf16_to_f32((uint16_t)(w.y >> 16));
+        vv[db][0] = h16_to_f32<H16>((uint16_t)(w.x & 0xffff));
+        vv[db][1] = h16_to_f32<H16>((uint16_t)(w.x >> 16));
+        vv[db][2] = h16_to_f32<H16>((uint16_t)(w.y & 0xffff));
+        vv[db][3] = h16_to_f32<H16>((uint16_t)(w.y >> 16));
       }
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   }
 
   // ---- epilogue: O[q][d = db*16 + 4g + i] = ot / l
-  if (out_mx) {
+  if (!H16 && out_mx) {
     // MX fp8 output (config C5, the out-proj input): one head = one 64-column block,
     // held by the 4 lanes {c, c+16, c+32, c+48}: block max over them, e8m0 scale,
     // RNE e4m3, 4x4 dword transpose so lane g owns columns 16g..16g+15 -> 16-B stores
@@ -417,8 +419,8 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
         uint2 r;
-        r.x = pack_bf16x2(ot[qb][db][0] * inv, ot[qb][db][1] * inv);
-        r.y = pack_bf16x2(ot[qb][db][2] * inv, ot[qb][db][3] * inv);
+        r.x = pack_h16x2<H16>(ot[qb][db][0] * inv, ot[qb][db][1] * inv);
+        r.y = pack_h16x2<H16>(ot[qb][db][2] * inv, ot[qb][db][3] * inv);
         *(uint2*)(o + db * 16 + 4 * g) = r;
       }
     }
@@ -497,17 +499,22 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(const float* __restrict__ 
 extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
                                 int heads, int head_dim, int flags, void* out_mx, int64_t ld_mx,
                                 void* stream) {
-  AACLIP_REQUIRE(dtype == AACLIP_F32 || dtype == AACLIP_BF16 || dtype == AACLIP_FP8);
+  AACLIP_REQUIRE(dtype == AACLIP_F32 || dtype == AACLIP_BF16 || dtype == AACLIP_FP8 || dtype == AACLIP_F16);
   AACLIP_REQUIRE(qkv && out && batch > 0 && seq > 0 && heads > 0 && head_dim == HD_);
   AACLIP_REQUIRE((flags & ~(AACLIP_ATTN_CAUSAL | AACLIP_ATTN_Q_PRESCALED)) == 0);
   AACLIP_REQUIRE(dtype != AACLIP_F32 || !(flags & AACLIP_ATTN_Q_PRESCALED));
   AACLIP_REQUIRE((int64_t)batch * seq * 3 * heads * HD_ * 2 < (1ll << 31));  // buffer-descriptor range
   AACLIP_REQUIRE(dtype != AACLIP_FP8 || (out_mx && ld_mx >= (int64_t)batch * seq && heads % 2 == 0));
   hipStream_t s = (hipStream_t)stream;
-  if (dtype != AACLIP_F32) {  // bf16 compute; fp8 = bf16 inputs with an MX e4m3 output
+  if (dtype == AACLIP_F16) {  // fp16 compute (parity-grade 16-bit mode)
     const long nwg = (long)ceil_div(seq, QT) * batch * heads;
     AACLIP_REQUIRE(nwg < (1L << 31));
-    attn_bf16_kernel<<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, batch, seq, heads,
+    attn_bf16_kernel<true><<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, batch, seq, heads,
+                                                         flags, nullptr, 0);
+  } else if (dtype != AACLIP_F32) {  // bf16 compute; fp8 = bf16 inputs with an MX e4m3 output
+    const long nwg = (long)ceil_div(seq, QT) * batch * heads;
+    AACLIP_REQUIRE(nwg < (1L << 31));
+    attn_bf16_kernel<false><<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, batch, seq, heads,
                                                    flags, dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr, ld_mx);
   } else {
     dim3 grid(ceil_div(seq, 64), batch * heads);

@@ -149,10 +149,11 @@ __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, i
 // i's stores (vmcnt retires in issue order).
 constexpr int EPI_REMAP = 64;
 
-__device__ __forceinline__ uint4 pair_bf16(const float4_t& lo, const float4_t& hi, int fq) {
+template <bool H16>
+__device__ __forceinline__ uint4 pair_h16(const float4_t& lo, const float4_t& hi, int fq) {
   // lo = this lane's 4 columns of tile j0, hi = of tile j1 (both row fr, cols 4fq..4fq+3)
-  uint32_t a0 = pack_bf16x2(lo[0], lo[1]), a1 = pack_bf16x2(lo[2], lo[3]);
-  uint32_t b0 = pack_bf16x2(hi[0], hi[1]), b1 = pack_bf16x2(hi[2], hi[3]);
+  uint32_t a0 = pack_h16x2<H16>(lo[0], lo[1]), a1 = pack_h16x2<H16>(lo[2], lo[3]);
+  uint32_t b0 = pack_h16x2<H16>(hi[0], hi[1]), b1 = pack_h16x2<H16>(hi[2], hi[3]);
   auto x = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
   auto y = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
   // fq even: tile j0 cols 8(fq/2)..+7; fq odd: tile j1 cols 8(fq/2)..+7
@@ -167,7 +168,8 @@ __device__ __forceinline__ uint4 pair_bf16(const float4_t& lo, const float4_t& h
 // groups, power-of-two scale, RNE to e4m3, 4x4 lane-group transpose -> 16-B stores.
 // SCALED: 0 = none, 1 = a_scale[row] * w_scale[col] (fp8 per-row), 2 = w_scale[col]
 // only (fp8 MX: the activation block scales were applied by the MFMA).
-template <int RM, int RN, int OUTM, int EPI, int SCALED>
+// H16: the 16-bit storage of OUTM 1 and of the aux copy is fp16 (else bf16).
+template <int RM, int RN, int OUTM, int EPI, int SCALED, bool H16 = false>
 __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
                                               int lane) {
   static_assert(RN % 2 == 0, "column tiles are paired");
@@ -248,7 +250,7 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
     uint4 pk[RN / 2];
     if (BF16OUT || (epi & AACLIP_EPI_AUX_BF16)) {
 #pragma unroll
-      for (int q = 0; q < RN / 2; ++q) pk[q] = pair_bf16(v[2 * q], v[2 * q + 1], fq);
+      for (int q = 0; q < RN / 2; ++q) pk[q] = pair_h16<H16>(v[2 * q], v[2 * q + 1], fq);
     }
     if (m < a.M) {
       if constexpr (BF16OUT) {
@@ -279,8 +281,10 @@ typedef __attribute__((ext_vector_type(4))) int i32x4_t;
 // Q: 0 = bf16, 1 = fp8 with per-row A scales (epilogue), 2 = fp8 MX: A carries an
 // e8m0 scale per (row, 64-K block) staged through LDS next to the tiles and applied
 // by the MFMA's B-operand scale (the A tile is the MFMA's second operand).
-template <int BM, int BN, int WM, int WN, int Q = 0>
+// H16 (Q == 0 only): fp16 operands on v_mfma_f32_16x16x32_f16 (same tiles and cycles).
+template <int BM, int BN, int WM, int WN, int Q = 0, bool H16 = false>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
+  static_assert(!H16 || Q == 0, "fp16 operands: 16-bit path only");
   constexpr bool FP8 = Q != 0, MX = Q == 2;
   constexpr int NWAVES = WM * WN;
   constexpr int ES = FP8 ? 1 : 2;  // element bytes
@@ -409,15 +413,15 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
     } else {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t bf[RN];
+        using V8 = h16x8_t<H16>;
+        V8 bf[RN];
 #pragma unroll
-        for (int j = 0; j < RN; ++j) bf[j] = *(const bf16x8_t*)(base + b_off[j][kk]);
+        for (int j = 0; j < RN; ++j) bf[j] = *(const V8*)(base + b_off[j][kk]);
 #pragma unroll
         for (int i = 0; i < RM; ++i) {
-          const bf16x8_t af = *(const bf16x8_t*)(base + a_off[i][kk]);
+          const V8 af = *(const V8*)(base + a_off[i][kk]);
 #pragma unroll
-          for (int j = 0; j < RN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);  // C^T tile
+          for (int j = 0; j < RN; ++j) acc[i][j] = mfma16(bf[j], af, acc[i][j]);  // C^T tile
         }
       }
     }
@@ -435,10 +439,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   const int mw = m0 + wm * TM, nw = n0 + wn * TN;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
   constexpr int SC = Q == 1 ? 1 : (Q == 2 ? 2 : 0);
-  const int outm = a.out_dtype == AACLIP_F32 ? 0 : (a.out_dtype == AACLIP_BF16 ? 1 : 2);
+  const int outm = a.out_dtype == AACLIP_F32 ? 0 : (a.out_dtype == AACLIP_FP8 ? 2 : 1);
 #define EPI_CASE(OM, E)                                                \
   if (outm == (OM) && key == (E)) {                                    \
-    wave_epilogue<RM, RN, OM, E, SC>(a, acc, mw, nw, lane);            \
+    wave_epilogue<RM, RN, OM, E, SC, H16>(a, acc, mw, nw, lane);       \
     return;                                                            \
   }
   // the combinations the visual/text engines issue (engine.py)
@@ -454,9 +458,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   }
 #undef EPI_CASE
   if (outm == 1)
-    wave_epilogue<RM, RN, 1, -1, SC>(a, acc, mw, nw, lane);
+    wave_epilogue<RM, RN, 1, -1, SC, H16>(a, acc, mw, nw, lane);
   else if (outm == 0)
-    wave_epilogue<RM, RN, 0, -1, SC>(a, acc, mw, nw, lane);
+    wave_epilogue<RM, RN, 0, -1, SC, H16>(a, acc, mw, nw, lane);
 }
 
 // ============================================================== fp32 MFMA kernel
@@ -534,7 +538,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
 // Loads past the last K-step re-read its columns into regions nobody reads again,
 // so the vmcnt arithmetic stays uniform. Operands via buffer descriptors (rows >= M
 // read as zero; outputs dropped by the epilogue's bound check).
+template <bool H16>
 __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
+  using V8 = h16x8_t<H16>;
   constexpr int BM = 256, BN = 256, TM = 128, TN = 64, RM = 8, RN = 4;
   constexpr int REGION = 128 * 128;                 // bytes per LDS region
   constexpr int STAGE = 4 * REGION;                 // A0, A1, B0, B1
@@ -587,7 +593,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   for (int i = 0; i < RM; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-  bf16x8_t af[4][2], bfr[2][2][2];  // A sub-block (4 tiles x kk), B sub-blocks [q][j][kk]
+  V8 af[4][2], bfr[2][2][2];  // A sub-block (4 tiles x kk), B sub-blocks [q][j][kk]
 
   // prologue: all of K-step 0, then A0 / B0 of K-step 1 (the steady state's P3/P4 of K-step -1)
   issue(0, 0);
@@ -608,22 +614,21 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qa * 4 + i][qb * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[qb][j][kk], af[i][kk], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+          acc[qa * 4 + i][qb * 2 + j] = mfma16(bfr[qb][j][kk], af[i][kk], acc[qa * 4 + i][qb * 2 + j]);
     __builtin_amdgcn_s_setprio(0);
   };
   auto read_a = [&](const char* st, int q) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = *(const bf16x8_t*)(st + q * REGION + a_rd[kk] + i * 2048);
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = *(const V8*)(st + q * REGION + a_rd[kk] + i * 2048);
   };
   auto read_b = [&](const char* st, int q) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-        bfr[q][j][kk] = *(const bf16x8_t*)(st + q * REGION + b_rd[kk] + j * 2048);
+        bfr[q][j][kk] = *(const V8*)(st + q * REGION + b_rd[kk] + j * 2048);
   };
 #define PH_SYNC_MFMA(QA, QB)                                 \
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");           \
@@ -666,10 +671,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   const int mw = m0 + wr * TM, nw = n0 + wc * TN;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
   const bool bf16_out = a.out_dtype != AACLIP_F32;
-#define EPI_CASE(BF, E)                                            \
-  if (bf16_out == (BF) && key == (E)) {                            \
-    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0>(a, acc, mw, nw, lane); \
-    return;                                                        \
+#define EPI_CASE(BF, E)                                                 \
+  if (bf16_out == (BF) && key == (E)) {                                 \
+    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane); \
+    return;                                                             \
   }
   EPI_CASE(true, AACLIP_EPI_BIAS)
   EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)
@@ -678,9 +683,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   EPI_CASE(false, AACLIP_EPI_LEAKY)
 #undef EPI_CASE
   if (bf16_out)
-    wave_epilogue<RM, RN, 1, -1, 0>(a, acc, mw, nw, lane);
+    wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane);
   else
-    wave_epilogue<RM, RN, 0, -1, 0>(a, acc, mw, nw, lane);
+    wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane);
 }
 
 // ============================ 8-phase ping-pong fp8 MX kernel (256x256, K-step 128)
@@ -865,27 +870,29 @@ int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
   return AACLIP_OK;
 }
 
+template <bool H16>
 int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   if (a.N % 256 || a.K % 64) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
   const size_t lds = 2 * 4 * 128 * 128;
   static unsigned attr_dev = 0;
-  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
-  gemm_bf16_8ph_kernel<<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
+  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16>, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
+  gemm_bf16_8ph_kernel<H16><<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
 
-template <int BM, int BN, int WM, int WN, int Q = 0>
+template <int BM, int BN, int WM, int WN, int Q = 0, bool H16 = false>
 int launch_bf16(GemmArgs a, hipStream_t s) {
   if (a.N % BN) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, BM);
   a.tiles_n = a.N / BN;
   const size_t lds = 2 * (size_t)(BM + BN) * 128 + (Q == 2 ? 2 * BM * 2 : 0);
   static unsigned attr_dev = 0;
-  if (!lds_attr_once((const void*)gemm_bf16_kernel<BM, BN, WM, WN, Q>, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
-  gemm_bf16_kernel<BM, BN, WM, WN, Q><<<a.tiles_m * a.tiles_n, WM * WN * 64, lds, s>>>(a);
+  if (!lds_attr_once((const void*)gemm_bf16_kernel<BM, BN, WM, WN, Q, H16>, (int)lds, attr_dev))
+    return AACLIP_ERR_LAUNCH;
+  gemm_bf16_kernel<BM, BN, WM, WN, Q, H16><<<a.tiles_m * a.tiles_n, WM * WN * 64, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -922,12 +929,46 @@ int g_group_m = 8;
 int g_setprio = 0;
 int g_dbg = 0;
 
+// 16-bit dispatch (bf16 or fp16 operands; same tiles, same per-shape choice)
+template <bool H16>
+int dispatch16(GemmArgs a, hipStream_t s) {
+  const int M = a.M, N = a.N;
+  if (a.K % 64 || N % 128) return AACLIP_ERR_ARG;
+  const bool fits = (int64_t)M * a.lda * 2 < (1ll << 31) && (int64_t)N * a.ldw * 2 < (1ll << 31);
+  switch (g_gemm_variant) {
+    case 1: return launch_bf16<256, 256, 2, 4, 0, H16>(a, s);
+    case 2: return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
+    case 3:
+    case 4:  // 8-phase for the wide GEMMs only (N >= 2048), 320x256 below
+      if (N % 256 == 0 && (g_gemm_variant == 3 || N >= 2048) && fits) return launch_bf16_8ph<H16>(a, s);
+      break;
+    case 9: return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);  // 128x128 everywhere (A/B)
+    case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
+      if (N % 256 == 0) return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
+      break;
+    default: break;
+  }
+  // Default: per shape, the kernel with the fewer tile rounds weighted by its per-tile
+  // cost. M = B*577 tiles unevenly: 320-row tiles of the LDS-DMA kernel vs 256-row
+  // tiles of the 8-phase kernel (~10 % faster per FLOP). E.g. in the two-stream
+  // pipeline (16 images per stream, M = 9232) the 8-phase kernel wins on QKV, out-proj,
+  // c_proj and adapters (148-444 tiles) and the 320-row one on c_fc (464 vs 592 tiles
+  // = 2 vs 3 rounds); measured per shape with tools/kbench.py, whole C2 step +5 %.
+  if (N % 256 == 0 && g_gemm_variant == 0) {
+    const bool ph8 = fits && prefer_8ph(M, N);
+    if (prefer_small(M, N, ph8)) return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);
+    if (ph8) return launch_bf16_8ph<H16>(a, s);
+  }
+  if (N % 256 == 0) return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
+  return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
+}
+
 }  // namespace
 
 // Which kernel aaclip_gemm launches for this shape (same decision as the dispatch
 // below; for reports such as bench.py's roofline label). Host only.
 extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
-  if (in_dtype != AACLIP_BF16) return "gemm_f32_kernel";
+  if (in_dtype != AACLIP_BF16 && in_dtype != AACLIP_F16) return "gemm_f32_kernel";
   if (M <= 0 || N % 128 || K % 64) return "invalid";
   switch (g_gemm_variant) {
     case 1: return "gemm_bf16_kernel<256,256,2,4>";
@@ -969,8 +1010,9 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
                            int epilogue, const float* bias, const float* residual, int64_t ldr,
                            void* aux, int64_t ldaux, int row_group, int row_group_out,
                            int row_offset, void* stream) {
-  AACLIP_REQUIRE(in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16);
-  AACLIP_REQUIRE(out_dtype == AACLIP_F32 || out_dtype == AACLIP_BF16);
+  AACLIP_REQUIRE(in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16 || in_dtype == AACLIP_F16);
+  AACLIP_REQUIRE(out_dtype == AACLIP_F32 || (in_dtype != AACLIP_F32 && out_dtype == in_dtype) ||
+                 (in_dtype == AACLIP_F32 && out_dtype == AACLIP_BF16));
   AACLIP_REQUIRE(A && W && C && M >= 0 && N > 0 && K > 0);
   AACLIP_REQUIRE(lda >= K && ldw >= K && ldc >= N && lda % 8 == 0 && ldw % 8 == 0 && ldc % 4 == 0);
   AACLIP_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0 && ((uintptr_t)C % 16) == 0);
@@ -984,37 +1026,8 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
              out_dtype, row_group, row_group_out, row_offset, 0, 0, g_group_m, g_setprio, g_dbg,
              nullptr, nullptr, nullptr, 0, nullptr, 0};
   hipStream_t s = (hipStream_t)stream;
-  if (in_dtype == AACLIP_BF16) {
-    AACLIP_REQUIRE(K % 64 == 0 && N % 128 == 0);
-    switch (g_gemm_variant) {
-      case 1: return launch_bf16<256, 256, 2, 4>(a, s);
-      case 2: return launch_bf16<256, 128, 4, 2>(a, s);
-      case 3:
-      case 4:  // 8-phase for the wide GEMMs only (N >= 2048), 320x256 below
-        if (N % 256 == 0 && (g_gemm_variant == 3 || N >= 2048) && (int64_t)M * lda * 2 < (1ll << 31) &&
-            (int64_t)N * ldw * 2 < (1ll << 31))
-          return launch_bf16_8ph(a, s);
-        break;
-      case 9: return launch_bf16<128, 128, 2, 2>(a, s);  // 128x128 everywhere (A/B)
-      case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
-        if (N % 256 == 0) return launch_bf16<320, 256, 2, 4>(a, s);
-        break;
-      default: break;
-    }
-    // Default: per shape, the kernel with the fewer tile rounds weighted by its per-tile
-    // cost. M = B*577 tiles unevenly: 320-row tiles of the LDS-DMA kernel vs 256-row
-    // tiles of the 8-phase kernel (~10 % faster per FLOP). E.g. in the two-stream
-    // pipeline (16 images per stream, M = 9232) the 8-phase kernel wins on QKV, out-proj,
-    // c_proj and adapters (148-444 tiles) and the 320-row one on c_fc (464 vs 592 tiles
-    // = 2 vs 3 rounds); measured per shape with tools/kbench.py, whole C2 step +5 %.
-    if (N % 256 == 0 && g_gemm_variant == 0) {
-      const bool ph8 = (int64_t)M * lda * 2 < (1ll << 31) && (int64_t)N * ldw * 2 < (1ll << 31) && prefer_8ph(M, N);
-      if (prefer_small(M, N, ph8)) return launch_bf16<128, 128, 2, 2>(a, s);
-      if (ph8) return launch_bf16_8ph(a, s);
-    }
-    if (N % 256 == 0) return launch_bf16<320, 256, 2, 4>(a, s);
-    return launch_bf16<256, 128, 4, 2>(a, s);
-  }
+  if (in_dtype == AACLIP_BF16) return dispatch16<false>(a, s);
+  if (in_dtype == AACLIP_F16) return dispatch16<true>(a, s);
   AACLIP_REQUIRE(K % 16 == 0 && N % 64 == 0);
   a.tiles_m = ceil_div(M, 64);
   a.tiles_n = N / 64;

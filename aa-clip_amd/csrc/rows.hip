@@ -22,6 +22,16 @@ template <int VEC>
 __device__ __forceinline__ void load_any(const void* p, int dtype, float4_t (&v)[VEC], int lane) {
   if (dtype == AACLIP_F32) {
     load_f32<VEC>((const float*)p, v, lane);
+  } else if (dtype == AACLIP_F16) {
+    const uint16_t* q = (const uint16_t*)p;
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) {
+      uint2 r = *(const uint2*)(q + 256 * c + 4 * lane);
+      v[c][0] = f16_to_f32((uint16_t)(r.x & 0xffff));
+      v[c][1] = f16_to_f32((uint16_t)(r.x >> 16));
+      v[c][2] = f16_to_f32((uint16_t)(r.y & 0xffff));
+      v[c][3] = f16_to_f32((uint16_t)(r.y >> 16));
+    }
   } else {
     const uint16_t* q = (const uint16_t*)p;
 #pragma unroll
@@ -41,12 +51,13 @@ __device__ __forceinline__ void store_any(void* p, int dtype, const float4_t (&v
 #pragma unroll
     for (int c = 0; c < VEC; ++c) *(float4_t*)((float*)p + 256 * c + 4 * lane) = v[c];
   } else {
+    const bool h = dtype == AACLIP_F16;
     uint16_t* q = (uint16_t*)p;
 #pragma unroll
     for (int c = 0; c < VEC; ++c) {
       uint2 r;
-      r.x = pack_bf16x2(v[c][0], v[c][1]);
-      r.y = pack_bf16x2(v[c][2], v[c][3]);
+      r.x = h ? pack_f16x2(v[c][0], v[c][1]) : pack_bf16x2(v[c][0], v[c][1]);
+      r.y = h ? pack_f16x2(v[c][2], v[c][3]) : pack_bf16x2(v[c][2], v[c][3]);
       *(uint2*)(q + 256 * c + 4 * lane) = r;
     }
   }
@@ -89,7 +100,7 @@ __device__ __forceinline__ void layer_norm(const float4_t (&x)[VEC], const float
   }
 }
 
-__device__ __forceinline__ size_t esize(int dtype) { return dtype == AACLIP_F32 ? 4 : (dtype == AACLIP_BF16 ? 2 : 1); }
+__device__ __forceinline__ size_t esize(int dtype) { return dtype == AACLIP_F32 ? 4 : (dtype == AACLIP_FP8 ? 1 : 2); }
 
 // smallest e with amax * 2^-e <= 448 (largest finite e4m3): the e8m0 block scale
 __device__ __forceinline__ int mx_exp_row(float amax) {
@@ -191,7 +202,7 @@ __global__ __launch_bounds__(256) void block_tail_kernel(int out_dtype, float* x
     layer_norm<VEC>(v, lw, lb, y, lane);
     store_out<VEC>(h, out_dtype, row, sc, ld_sc, y, lane);
   }
-  if (tap) {  // level taps stay bf16/fp32 (seg_proj inputs) when h is fp8
+  if (tap) {  // level taps stay bf16 (seg_proj inputs) when h is fp8
     const int tdt = out_dtype == AACLIP_FP8 ? AACLIP_BF16 : out_dtype;
     const int t = row % n_tok;
     if (t >= 1) {
@@ -345,6 +356,13 @@ __global__ __launch_bounds__(256) void im2col_kernel(int out_dtype, const float*
     float* o = (float*)cols + row * kp + kc * 8;
     *(float4_t*)o = float4_t{v[0], v[1], v[2], v[3]};
     *(float4_t*)(o + 4) = float4_t{v[4], v[5], v[6], v[7]};
+  } else if (out_dtype == AACLIP_F16) {
+    uint4 r;
+    r.x = pack_f16x2(v[0], v[1]);
+    r.y = pack_f16x2(v[2], v[3]);
+    r.z = pack_f16x2(v[4], v[5]);
+    r.w = pack_f16x2(v[6], v[7]);
+    *(uint4*)((uint16_t*)cols + row * kp + kc * 8) = r;
   } else {
     uint4 r;
     r.x = pack_bf16x2(v[0], v[1]);
@@ -362,7 +380,7 @@ __global__ __launch_bounds__(256) void im2col_kernel(int out_dtype, const float*
     default: return AACLIP_ERR_ARG;              \
   }
 
-inline bool dtype_ok(int d) { return d == AACLIP_F32 || d == AACLIP_BF16; }
+inline bool dtype_ok(int d) { return d == AACLIP_F32 || d == AACLIP_BF16 || d == AACLIP_F16; }
 // fp8 MX outputs (config C5) need the e8m0 scale buffer [width/128][ld_mx >= rows][2]
 inline bool mx_ok(int d, const void* mx, int64_t ld_mx, int rows, int width) {
   return dtype_ok(d) || (d == AACLIP_FP8 && mx && ld_mx >= rows && width % 128 == 0);
@@ -556,7 +574,7 @@ extern "C" int aaclip_im2col(int out_dtype, const float* img, void* cols, int ba
 
 extern "C" int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int64_t ldq, float* scale,
                                      int rows, int cols, void* stream) {
-  AACLIP_REQUIRE(dtype_ok(in_dtype) && x && q && scale && rows >= 0 && cols > 0 && cols % 8 == 0);
+  AACLIP_REQUIRE((in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16) && x && q && scale && rows >= 0 && cols > 0 && cols % 8 == 0);
   AACLIP_REQUIRE(ldx >= cols && ldq >= cols && ldx % 8 == 0 && ldq % 8 == 0);
   AACLIP_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)q % 8) == 0);
   if (rows == 0) return AACLIP_OK;
@@ -568,7 +586,7 @@ extern "C" int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, v
 
 extern "C" int aaclip_quant_fp8_mx(int in_dtype, const void* x, int64_t ldx, void* q, int64_t ldq, void* sc,
                                    int64_t ld_sc, int rows, int cols, void* stream) {
-  AACLIP_REQUIRE(dtype_ok(in_dtype) && x && q && sc && rows >= 0 && cols > 0 && cols % 128 == 0);
+  AACLIP_REQUIRE((in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16) && x && q && sc && rows >= 0 && cols > 0 && cols % 128 == 0);
   AACLIP_REQUIRE(ldx >= cols && ldq >= cols && ldx % 8 == 0 && ldq % 8 == 0 && ld_sc >= rows);
   AACLIP_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)q % 8) == 0);
   if (rows == 0) return AACLIP_OK;

@@ -8,8 +8,9 @@ parameters; the packed device copies are rebuilt whenever a parameter changes
 (load_state_dict, in-place edits: tracked by tensor version counters).
 
 Compute dtype of the visual tower: bf16 MFMA by default (`compute_dtype=
-torch.float32` selects the fp32-MFMA parity mode, `torch.float8_e4m3fn` the config-C5
-fp8 MX mode; env AACLIP_DTYPE=fp32 / fp8 too).
+torch.float16` selects the fp16-MFMA mode that meets the north_star map contract
+at the bf16 rate, `torch.float32` the fp32-MFMA parity mode, `torch.float8_e4m3fn`
+the config-C5 fp8 MX mode; env AACLIP_DTYPE=fp16 / fp32 / fp8 too).
 The text tower always runs fp32 (once per dataset, <1% of the work).
 """
 from __future__ import annotations
@@ -31,7 +32,13 @@ def _default_dtype():
     v = os.environ.get("AACLIP_DTYPE", "bf16").lower()
     if v in ("fp8", "float8", "e4m3"):  # config C5: fp8 MX block GEMMs
         return torch.float8_e4m3fn
-    return torch.float32 if v in ("fp32", "float32", "f32") else torch.bfloat16
+    if v in ("fp16", "float16", "f16", "half"):  # parity-grade 16-bit mode (fp16 MFMA)
+        return torch.float16
+    if v in ("fp32", "float32", "f32"):
+        return torch.float32
+    if v in ("bf16", "bfloat16"):
+        return torch.bfloat16
+    raise ValueError(f"AACLIP_DTYPE={v!r}: expected bf16, fp16, fp32 or fp8")
 
 
 class AdaptedCLIP(nn.Module):

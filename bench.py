@@ -28,11 +28,36 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "aa-clip_amd"))
 sys.path.insert(0, ROOT)
 
+
+def _self_launch():
+    """`python bench.py --gpus N` with no torchrun environment: start the N ranks
+    ourselves (torch.distributed.run as a CHILD process, one rank per GPU over
+    RCCL) and exit with its code. Runs before torch is imported, so this parent
+    never touches the GPU (no exec from a GPU-initialised process)."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    known, _ = ap.parse_known_args()
+    if known.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.run(cmd).returncode)
+
+
+if __name__ == "__main__":
+    _self_launch()
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from aaclip import ops  # noqa: E402
 from aaclip.engine import HEADS, LAYERS, WIDTH, VisualEngine  # noqa: E402
+from aaclip.parallel import shard_range, sharded_step  # noqa: E402
 
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -257,47 +282,89 @@ def c5_leg(dev, steps: int, warmup: int, streams: int, batch: int = 32):
     return out
 
 
-def cpu_baseline_and_parity(n_images: int, dev, streams: int):
-    """CPU leg on rank 0: the numpy oracle (fp32 restatement of the reference,
-    pinned to its golden vectors) timed on this host's cores over a bounded
-    sample (forward + 4-level map + image score per image), and the same images
-    through the GPU path with the SAME synthetic weights -> map error and
-    pixel-AUROC parity (sklearn roc_auc_score over seeded anomaly masks)."""
+def _host_cores():
+    """(nproc, physical cores from lscpu) of this host, for the record."""
+    import subprocess
+    nproc = os.cpu_count() or 1
+    phys = None
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        phys = len({ln for ln in out.splitlines() if ln and not ln.startswith("#")}) or None
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return nproc, phys
+
+
+def cpu_baseline_and_parity(dev, streams: int, min_seconds: float = 12.0, warmup: int = 2, parity_images: int = 4):
+    """CPU leg on rank 0: the numpy oracle (fp32 restatement of the
+    reference, pinned to its golden vectors) runs the per-batch path — forward +
+    4-level map + image score, bs = 1 — on this host's cores: 2 warm-up batches,
+    then >= min_seconds of steady state, at 4 threads (the reference's own setting,
+    test.py:28-35) and at every core this job may use. The first images' maps and
+    scores are also the parity reference for the GPU modes (same synthetic
+    weights/images/masks): max map error, fraction of pixels inside the north_star
+    envelope, pixel-AUROC (sklearn) and image labels."""
     import numpy as np
     from sklearn.metrics import roc_auc_score
+    from threadpoolctl import threadpool_limits
 
     from oracle import aaclip_np as R
     from oracle import synth
     sd = synth.clip_state_dict(111)
     ia, _ = synth.adapter_state_dicts(111)
-    x = synth.images(111, n_images, 336)
-    masks = synth.masks(111, n_images, 336)[:, 0]
     T = np.linalg.qr(np.random.default_rng(0).standard_normal((768, 2)))[0].astype(np.float32)
-    R.visual_forward(sd, ia, x[:1])  # warm-up (BLAS threads, page-in)
-    t0 = time.perf_counter()
-    ref_maps, ref_scores = [], []
-    for i in range(n_images):
+    pool = 64
+    x = synth.images(111, pool, 336)
+    nproc, phys = _host_cores()
+    allowed = int(os.environ.get("OMP_NUM_THREADS", nproc))
+    ref = {}
+
+    def one(i):
         seg, det = R.visual_forward(sd, ia, x[i:i + 1])
-        ref_maps.append(R.anomaly_map(seg, T, 336, "Industrial"))
-        ref_scores.append(R.image_score(det, T))
-    dt = time.perf_counter() - t0
-    ref_maps, ref_scores = np.concatenate(ref_maps), np.concatenate(ref_scores)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    base = {"value": round(n_images / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"{n_images} synthetic 336px images, bs=1, fp32 numpy oracle of the reference "
-                      f"(oracle/aaclip_np.py) on {threads} host threads, {dt:.1f} s"}
+        m, sc = R.anomaly_map(seg, T, 336, "Industrial"), R.image_score(det, T)
+        if i < parity_images and i not in ref:
+            ref[i] = (m, sc)
+
+    legs = {}
+    for threads in sorted({4, allowed}):
+        with threadpool_limits(limits=threads):
+            for i in range(warmup):
+                one(i)
+            n, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < min_seconds or n < parity_images:
+                one((warmup + n) % pool)
+                n += 1
+            dt = time.perf_counter() - t0
+        legs[threads] = {"value": round(n / dt, 4), "images": n, "seconds": round(dt, 2)}
+    main_t = allowed if allowed in legs else max(legs)
+    base = {"value": legs[main_t]["value"], "unit": "images/sec", "cores": main_t, "kind": "port",
+            "threads_4": legs.get(4), f"threads_{main_t}": legs[main_t],
+            "host": {"nproc": nproc, "physical_cores_lscpu": phys, "threads_allowed": allowed},
+            "sample": (f"fp32 numpy oracle of the reference (oracle/aaclip_np.py), bs=1 synthetic 336px images "
+                       f"through forward + 4-level map + image score; {warmup} warm-up batches then >= "
+                       f"{min_seconds:.0f} s steady state per leg; legs at 4 threads (reference test.py:28-35) "
+                       f"and {main_t} threads (the cores this job may use; 'value')")}
+    # parity of each GPU mode against the CPU reference on the first images
+    n = parity_images
+    for i in range(n):
+        if i not in ref:
+            one(i)
+    ref_maps = np.concatenate([ref[i][0] for i in range(n)])
+    ref_scores = np.concatenate([ref[i][1] for i in range(n)])
+    masks = synth.masks(111, n, 336)[:, 0]
     vp = {k: torch.from_numpy(v).to(dev) for k, v in sd.items() if k.startswith("visual.")}
     iad = {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}
     lab = masks.reshape(-1) > 0
     auc_cpu = float(roc_auc_score(lab, ref_maps.reshape(-1)))
     tol = 1e-3 + 1e-2 * np.abs(ref_maps)
-    parity = {"images": n_images, "pixel_auroc_cpu_ref": round(auc_cpu, 6),
+    parity = {"images": n, "pixel_auroc_cpu_ref": round(auc_cpu, 6),
               "tolerance": "maps |gpu - ref| <= 1e-3 + 1e-2*|ref| (north_star)",
               "reference": "CPU fp32 numpy oracle (pinned to the reference's golden vectors), same "
                            "synthetic weights/images/masks"}
-    for tag, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+    xs = torch.from_numpy(x[:n]).to(dev)
+    for tag, dt in (("bf16", torch.bfloat16), ("fp16", torch.float16), ("fp32", torch.float32)):
         eng = VisualEngine(vp, iad, dtype=dt)
-        m, s = eng.predict(torch.from_numpy(x).to(dev), torch.from_numpy(T).to(dev), "Industrial", streams=streams)
+        m, s = eng.predict(xs, torch.from_numpy(T).to(dev), "Industrial", streams=streams)
         gpu_maps, gpu_scores = m.cpu().numpy(), s.cpu().numpy()
         err = np.abs(gpu_maps - ref_maps)
         auc_gpu = float(roc_auc_score(lab, gpu_maps.reshape(-1)))
@@ -310,6 +377,30 @@ def cpu_baseline_and_parity(n_images: int, dev, streams: int):
     return base, parity
 
 
+def modes_leg(vp, ad, x, T, steps: int, warmup: int, streams: int):
+    """The C2 step (same weights, images, graph) in the other compute modes:
+    fp16 (fp16 MFMA, same rate as bf16, 8x finer operand rounding: the mode that
+    meets the north_star map contract) and fp32 (fp32 MFMA parity mode)."""
+    out = {}
+    B, S = x.shape[0], x.shape[-1]
+    for tag, dt, k in (("fp16", torch.float16, steps), ("fp32", torch.float32, max(2, steps // 5))):
+        eng = VisualEngine(vp, ad, dtype=dt)
+        run = eng.graphed_predict(B, S, "Industrial", streams=streams)
+        for _ in range(warmup):
+            run(x, T)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            run(x, T)
+        torch.cuda.synchronize()
+        dt_s = time.perf_counter() - t0
+        out[tag] = {"images_per_sec": round(B * k / dt_s, 2), "ms_per_step": round(dt_s / k * 1e3, 3), "steps": k,
+                    "tflops_whole_path": round(flops_per_image((S // 14) ** 2 + 1) * B * k / dt_s / 1e12, 1)}
+        del eng, run
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -317,17 +408,22 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
     ap.add_argument("--img-size", type=int, default=336)
-    ap.add_argument("--cpu-images", type=int, default=4, help="images for the CPU baseline + parity (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="steady-state seconds per CPU-baseline leg (0 = skip the CPU leg and parity)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="concurrent image chunks per GPU (HIP streams)")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-C5 leg (448 px, 6 levels, fp8)")
+    ap.add_argument("--no-modes", action="store_true", help="skip the fp16 / fp32 mode throughput leg")
     ap.add_argument("--gemm-variant", type=int, default=0, help="aaclip_set_gemm_variant value (A/B runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU "
+                 "(plain `python bench.py --gpus N` starts them itself)")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -339,23 +435,26 @@ def main():
         _lib.call("aaclip_set_gemm_variant", args.gemm_variant)
     vp, ad = synthetic_visual_weights(dev)
     eng = VisualEngine(vp, ad, dtype=torch.bfloat16)
-    del vp
     B, S = args.batch, args.img_size
-    g = torch.Generator(device=dev).manual_seed(111 + rank)
-    x = torch.randn(B, 3, S, S, device=dev, generator=g)
+    # one global batch of B * world images (the same seeded tensor on every rank);
+    # each rank owns its shard_range slice (C3: 256 = 8 x 32), weights replicated
+    n_total = B * world
+    g = torch.Generator(device=dev).manual_seed(111)
+    x_global = torch.randn(n_total, 3, S, S, device=dev, generator=g)
     T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
-    gathered = torch.empty(world * B, device=dev) if world > 1 else None
+    a, b = shard_range(n_total, rank, world)
+    x = x_global[a:b].contiguous()
+    del x_global
 
     run = None if args.no_graph else eng.graphed_predict(B, S, "Industrial", streams=args.streams)
 
-    def step():
+    def predict(xl, Tl):
         if run is not None:
-            maps, score = run(x, T)
-        else:
-            maps, score = eng.predict(x, T, "Industrial", streams=args.streams)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, score)
-        return maps
+            return run(xl, Tl)
+        return eng.predict(xl, Tl, "Industrial", streams=args.streams)
+
+    def step():
+        return sharded_step(predict, x, T, n_total)
 
     for _ in range(args.warmup):
         step()
@@ -376,7 +475,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    images = B * world * args.steps
+    images = n_total * args.steps
     ms_per_step = elapsed / args.steps * 1e3
     ws = eng._workspace(B, S)
     line = {
@@ -394,8 +493,9 @@ def main():
         "data": "synthetic (N(0,1) images on device, random-init ViT-L/14-336 + adapters)",
         "config": {"workload": "C2: AA-CLIP anomaly-map inference, ViT-L/14-336, bf16, 4 levels, 2 anchors, "
                                "Industrial blur, per-GPU batch of images",
-                   "global_batch": B * world, "img_size": S, "per_gpu_batch": B,
-                   "parallelism": f"image-sharded dp{world} (+RCCL all-gather of image scores)",
+                   "global_batch": n_total, "img_size": S, "per_gpu_batch": B,
+                   "parallelism": f"image-sharded dp{world} (shard_range slices of one global batch "
+                                  "+ RCCL all-gather of image scores)",
                    "streams_per_gpu": args.streams, "hipgraph": not args.no_graph,
                    "gflop_per_image": round(flops_per_image((S // 14) ** 2 + 1) / 1e9, 2)},
     }
@@ -404,12 +504,16 @@ def main():
         line["roofline"] = roofline_gemm(eng, ws)
         line["roofline_map"] = roofline_map(eng, ws, T)
         line["latency_b1"] = latency_b1(eng, S, T)
-    if rank == 0 and world == 1 and args.cpu_images > 0:
-        line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(args.cpu_images, dev, args.streams)
+    if rank == 0 and world == 1 and not args.no_modes:
+        del run
+        run = None
+        line["modes"] = modes_leg(vp, ad, x, T, args.steps, args.warmup, args.streams)
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(dev, args.streams, args.cpu_seconds)
     if rank == 0 and world == 1 and not args.no_roofline:
         line["preprocess"] = preprocess_leg(dev, B, S)
     if rank == 0 and world == 1 and not args.no_c5:
-        del eng, run
+        del eng, run, vp, ad
         torch.cuda.empty_cache()
         line["c5"] = c5_leg(dev, max(3, args.steps // 2), args.warmup, args.streams)
     if rank == 0:

@@ -10,7 +10,8 @@
  *     allocator owns them; nothing here allocates, frees or synchronises, so every
  *     call can be captured into a hipGraph). Row-major, leading dimensions in
  *     ELEMENTS. `stream` is a hipStream_t passed as void*.
- *   - dtype enums: AACLIP_F32 = 0, AACLIP_BF16 = 1. bf16 is stored as uint16.
+ *   - dtype enums: AACLIP_F32 = 0, AACLIP_BF16 = 1, AACLIP_FP8 = 2, AACLIP_F16 = 3.
+ *     bf16 / fp16 are stored as uint16.
  *
  * The reference (wei-paul/AA-CLIP) has no native code: each entry point below
  * replaces the PyTorch/kornia call sites cited next to it
@@ -34,13 +35,15 @@ extern "C" {
 #define AACLIP_F32 0
 #define AACLIP_BF16 1
 #define AACLIP_FP8 2   /* OCP e4m3 + e8m0 block scales (fp8 MX activations, config C5) */
+#define AACLIP_F16 3   /* IEEE fp16: the parity-grade 16-bit mode (fp16 MFMA, same rate as bf16) */
 
 /* GEMM epilogue flags (applied in this order) */
 #define AACLIP_EPI_BIAS 1      /* + bias[n] (fp32)                          */
 #define AACLIP_EPI_GELU 2      /* exact erf GELU (nn.GELU)                  */
 #define AACLIP_EPI_LEAKY 4     /* LeakyReLU(0.01) (nn.LeakyReLU)            */
 #define AACLIP_EPI_RESID 8     /* + residual[row, n] (fp32; may alias C)    */
-#define AACLIP_EPI_AUX_BF16 16 /* also store a bf16 copy of the result      */
+#define AACLIP_EPI_AUX_BF16 16 /* also store a 16-bit copy of the result: fp16 when
+                                  in_dtype is AACLIP_F16, bf16 otherwise      */
 
 /* ABI version (bumped on any signature change; 2 = MX fp8 LayerNorm outputs) and the target. */
 int aaclip_abi_version(void);
@@ -54,8 +57,9 @@ const char* aaclip_arch(void);
  * (transformer.py:359-365), adapter Linear+LeakyReLU (model/adapter_modules.py:6-26,
  * model/adapter.py:93), seg_proj/det_proj (adapter.py:107-110), text projection
  * (adapter.py:140, model/model.py:200).
- * in_dtype: A and W (bf16 -> bf16 MFMA, f32 -> f32 MFMA). out_dtype: C.
- * K % 64 == 0 (bf16) / K % 16 == 0 (f32); lda, ldw multiples of 8.
+ * in_dtype: A and W (bf16 -> bf16 MFMA, f16 -> f16 MFMA, f32 -> f32 MFMA).
+ * out_dtype: C, either f32 or the 16-bit in_dtype.
+ * K % 64 == 0 (bf16/f16) / K % 16 == 0 (f32); lda, ldw multiples of 8.
  * Output row remap when row_group > 0:
  *   out_row = (m / row_group) * row_group_out + row_offset + (m % row_group)
  * (used to write patch embeddings after each image's CLS slot). The same
