@@ -10,7 +10,7 @@ import ctypes
 import os
 
 LIB_PATH = os.environ.get("AACLIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaaclip_hip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 F32 = 0
 BF16 = 1
@@ -50,6 +50,7 @@ SIGNATURES = {
     "aaclip_anchor_reduce": [_P, _I, _I, _P, _I, _I, _P],
     "aaclip_l2_normalize": [_I, _I, _P, _L, _P, _L, _I, _I, _P],
     "aaclip_patch_scores": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _I, _P, _P],
+    "aaclip_patch_logits": [_I, _P, _L, _P, _I, _I, _I, _I, _P, _P],
     "aaclip_blur_upsample": [_P, _P, _I, _I, _I, _I, _I, _F, _I, _P],
     "aaclip_anomaly_map": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P],
     "aaclip_image_score": [_I, _P, _L, _P, _I, _I, _I, _I, _P, _P, _P, _P],

@@ -28,12 +28,25 @@ from . import ops
 WIDTH = 1024
 HEADS = 16
 Q_LOG2_SCALE = 0.125 * 1.4426950408889634  # 1/sqrt(64) * log2(e)
-WS_KEEP = 8  # resident per-chunk workspaces (per image size)
+WS_KEEP = 16  # resident per-chunk workspaces (per image size)
+MAX_STREAMS = 8  # concurrent image chunks per predict (<= WS_KEEP / 2: two chunk sizes per stream)
 LAYERS = 24
 PATCH = 14
 EMBED = 768
 KPATCH = 640  # 3*14*14 = 588 padded to a multiple of 64
 DOMAIN_BLUR = {"Industrial": (7, 1.0), "Medical": (9, 1.5)}
+
+
+def _on_device(fn):
+    """Run an engine entry point with its device current (ops launch on the current
+    device's stream; an engine on cuda:1 must not launch on cuda:0's)."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrap(self, *a, **k):
+        with torch.cuda.device(self.device):
+            return fn(self, *a, **k)
+    return wrap
 
 
 def _blur_for(domain: str):
@@ -194,6 +207,7 @@ class VisualEngine:
 
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
+    @_on_device
     def forward_raw(self, x: torch.Tensor, slot: int = 0):
         """Run the visual tower; returns (seg_raw list of [B*P, 768] views,
         det_raw [B*P, 768] view, workspace). Rows are unnormalised projections."""
@@ -278,20 +292,35 @@ class VisualEngine:
         det = sb[:, L * EMBED:]
         return seg, det, ws
 
+    @staticmethod
+    def max_chunk(img_size: int) -> int:
+        """Most images one forward_raw may take: the attention kernel addresses a
+        chunk's packed qkv through one buffer descriptor (< 2^31 bytes), i.e.
+        B * n_tok * 3 * 1024 * 2 B (606 images at 336 px, 254 at 518). Larger
+        batches are split into chunks of at most this many images."""
+        n_tok = (img_size // PATCH) ** 2 + 1
+        return max(1, ((1 << 31) - 1) // (n_tok * 3 * WIDTH * 2))
+
     @torch.no_grad()
+    @_on_device
     def forward(self, x: torch.Tensor):
-        """AdaptedCLIP.forward contract: (list[L] of [B,P,768] unit rows, det [B,768]) fp32."""
-        seg_raw, det_raw, ws = self.forward_raw(x)
-        B = x.shape[0]
-        P = ws["P"]
-        out = []
-        for s in seg_raw:
-            y = torch.empty(B * P, EMBED, device=self.device, dtype=torch.float32)
-            ops.l2_normalize(s, y)
-            out.append(y.view(B, P, EMBED))
-        det = torch.empty(B, EMBED, device=self.device, dtype=torch.float32)
-        ops.image_score(det_raw, B, P, ws["partial"], det=det)
-        return out, det
+        """AdaptedCLIP.forward contract: (list[L] of [B,P,768] unit rows, det [B,768]) fp32
+        (fresh tensors; batches above max_chunk run as consecutive chunks)."""
+        B, S = x.shape[0], x.shape[-1]
+        mc = self.max_chunk(S)
+        out, det = None, None
+        for b0 in range(0, B, mc):
+            b1 = min(B, b0 + mc)
+            seg_raw, det_raw, ws = self.forward_raw(x[b0:b1])
+            P = ws["P"]
+            if out is None:
+                out = [torch.empty(B * P, EMBED, device=self.device, dtype=torch.float32) for _ in seg_raw]
+                det = torch.empty(B, EMBED, device=self.device, dtype=torch.float32)
+            for s_, y in zip(seg_raw, out):
+                ops.l2_normalize(s_, y[b0 * P:b1 * P])
+            ops.image_score(det_raw, b1 - b0, P, ws["partial"], det=det[b0:b1])
+        P = out[0].shape[0] // B
+        return [y.view(B, P, EMBED) for y in out], det
 
     def _chunk_streams(self, n: int):
         if len(getattr(self, "_streams", [])) < n:
@@ -299,7 +328,9 @@ class VisualEngine:
         return self._streams[:n]
 
     @torch.no_grad()
-    def predict(self, x: torch.Tensor, T: torch.Tensor, domain: str = "Industrial", streams: int = 1):
+    @_on_device
+    def predict(self, x: torch.Tensor, T: torch.Tensor, domain: str = "Industrial", streams: int = 1,
+                _slot0: int = 0):
         """Fused test path: (anomaly map [B,S,S] fp32, image score [B] fp32),
         = test.py:80-93 with the level sum ahead of blur+upsample.
 
@@ -307,74 +338,95 @@ class VisualEngine:
         own HIP stream with its own workspace: the GEMM tails of one chunk
         (tile counts that leave CUs idle in the last wave) are filled by another
         chunk's tiles. A tuple gives the chunk sizes explicitly (summing to B).
-        Outputs land in one [B,S,S] / [B] buffer."""
+        Batches above max_chunk(S) are cut into more chunks, round-robin over the
+        streams (chunks sharing a stream share its workspace, in stream order).
+        The outputs are ENGINE-OWNED buffers, overwritten by the next predict of the
+        same (B, S): clone them to keep them (test.py does)."""
         B, S = x.shape[0], x.shape[-1]
         T = T.to(self.device, torch.float32).contiguous()
         k, s = _blur_for(domain)
+        mc = self.max_chunk(S)
         if isinstance(streams, (tuple, list)):
             sizes = [int(v) for v in streams if int(v) > 0]
             if sum(sizes) != B:
                 raise ValueError(f"chunk sizes {tuple(streams)} do not sum to the batch {B}")
-            bounds = [0]
-            for v in sizes:
-                bounds.append(bounds[-1] + v)
-            streams = len(sizes)
+            if max(sizes) > mc:
+                raise ValueError(f"chunk of {max(sizes)} images exceeds max_chunk({S}) = {mc}")
+            if len(sizes) > MAX_STREAMS:
+                raise ValueError(f"at most {MAX_STREAMS} explicit chunks")
+            nstreams = len(sizes)
         else:
-            streams = max(1, min(int(streams), B))
-            bounds = [(B * i) // streams for i in range(streams + 1)]
-        if streams == 1:
-            seg_raw, det_raw, ws = self.forward_raw(x)
+            nstreams = max(1, min(int(streams), B, MAX_STREAMS))
+            nchunks = max(nstreams, -(-B // mc))
+            sizes = [(B * (i + 1)) // nchunks - (B * i) // nchunks for i in range(nchunks)]
+        bounds = [0]
+        for v in sizes:
+            bounds.append(bounds[-1] + v)
+        if len(sizes) == 1:
+            seg_raw, det_raw, ws = self.forward_raw(x, slot=_slot0)
             ops.anomaly_map(seg_raw, T, ws["map"], ws["grid"], g=ws["g"], ksize=k, sigma=s)
             ops.image_score(det_raw, B, ws["P"], ws["partial"], det=ws["det"], T=T, score=ws["score"])
             return ws["map"], ws["score"]
-        key = ("out", B, S)
+        key = ("out", B, S, _slot0)
         if key not in self._ws:
             self._ws[key] = (torch.empty(B, S, S, device=self.device), torch.empty(B, device=self.device))
         out_map, out_score = self._ws[key]
         x = x.to(self.device, torch.float32).contiguous()
         main = torch.cuda.current_stream(self.device)
-        if len(getattr(self, "_events", [])) < streams + 1:
-            self._events = [torch.cuda.Event() for _ in range(streams + 1)]
-        ready, done = self._events[0], self._events[1:streams + 1]
+        if len(getattr(self, "_events", [])) < nstreams + 1:
+            self._events = [torch.cuda.Event() for _ in range(nstreams + 1)]
+        ready, done = self._events[0], self._events[1:nstreams + 1]
         ready.record(main)
-        for i, st in enumerate(self._chunk_streams(streams)):
+        sts = self._chunk_streams(nstreams)
+        for st in sts:
+            st.wait_event(ready)
+        for i in range(len(sizes)):
             b0, b1 = bounds[i], bounds[i + 1]
+            st = sts[i % nstreams]
             with torch.cuda.stream(st):
-                st.wait_event(ready)
-                seg_raw, det_raw, ws = self.forward_raw(x[b0:b1], slot=i)
+                seg_raw, det_raw, ws = self.forward_raw(x[b0:b1], slot=_slot0 + i % nstreams)
                 ops.anomaly_map(seg_raw, T, out_map[b0:b1], ws["grid"], g=ws["g"], ksize=k, sigma=s)
                 ops.image_score(det_raw, b1 - b0, ws["P"], ws["partial"], det=ws["det"], T=T,
                                 score=out_score[b0:b1])
-                done[i].record(st)
-        for ev in done:
+        for st, ev in zip(sts, done):
+            ev.record(st)
             main.wait_event(ev)
         return out_map, out_score
 
     @torch.no_grad()
+    @_on_device
     def graphed_predict(self, batch: int, img_size: int, domain: str = "Industrial", streams: int = 1):
         """Capture predict() for a fixed (batch, size, domain, streams) into one hipGraph
         (torch.cuda.CUDAGraph records the C-ABI launches on the capturing stream and the
         chunk streams' fork/join). Returns fn(x, T) -> (map, score) that copies the
         inputs into static device buffers and replays the graph: no per-kernel host
-        launch cost (matters at small batch, e.g. config C1's bs=1)."""
+        launch cost (matters at small batch, e.g. config C1's bs=1). The graph runs in
+        workspaces of its own (a private slot range), so eager predict() calls of the
+        same shape never write into the buffers it replays into or returns."""
+        self._graphs = getattr(self, "_graphs", 0) + 1
+        slot0 = 1000 * self._graphs
         x_s = torch.zeros(batch, 3, img_size, img_size, device=self.device)
         T_s = torch.zeros(EMBED, 2, device=self.device)
         T_s[0, 0] = 1.0
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
+        before = set(self._ws)
         with torch.cuda.stream(side):  # warm-up: allocate workspaces, set kernel attributes
-            self.predict(x_s, T_s, domain, streams=streams)
+            self.predict(x_s, T_s, domain, streams=streams, _slot0=slot0)
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+        mine = {k: v for k, v in self._ws.items() if k not in before}  # the graph's own workspaces
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            out_map, out_score = self.predict(x_s, T_s, domain, streams=streams)
-        held = list(self._ws.values())  # the workspaces the graph replays into stay allocated
+            out_map, out_score = self.predict(x_s, T_s, domain, streams=streams, _slot0=slot0)
+        held = list(mine.values())  # kept alive by the graph even if the LRU drops their keys
+        dev = self.device
 
         def run(x: torch.Tensor, T: torch.Tensor):
-            x_s.copy_(x, non_blocking=True)
-            T_s.copy_(T, non_blocking=True)
-            graph.replay()
+            with torch.cuda.device(dev):
+                x_s.copy_(x, non_blocking=True)
+                T_s.copy_(T, non_blocking=True)
+                graph.replay()
             return out_map, out_score
 
         run.graph = graph
@@ -421,6 +473,7 @@ class TextEngine:
             self.w_out = cdt(params["text_projection"].t())  # x @ P == x . (P^T)^T
 
     @torch.no_grad()
+    @_on_device
     def encode(self, tokens: torch.Tensor) -> torch.Tensor:
         tokens = tokens.to(self.device, torch.int32).contiguous()
         n, ctx = tokens.shape
@@ -455,6 +508,7 @@ class TextEngine:
         return out
 
     @torch.no_grad()
+    @_on_device
     def class_anchor(self, tok_normal: torch.Tensor, tok_abnormal: torch.Tensor) -> torch.Tensor:
         """forward_utils.py:146-161 -> T [768, 2] (normal, abnormal)."""
         T = torch.empty(self.w_out.shape[0], 2, device=self.device, dtype=torch.float32)

@@ -37,9 +37,21 @@ def _ptr(t):
 
 
 def _dev(*ts):
+    """Every operand must be a device tensor on the CURRENT device: kernels launch on
+    the current device's stream (and the C side keys its per-device caches on
+    hipGetDevice), so a tensor on another GPU would be a wrong-device pointer. The
+    engines enter `torch.cuda.device(their device)` around every launch sequence."""
+    cur = None
     for t in ts:
-        if t is not None and not t.is_cuda:
+        if t is None:
+            continue
+        if not t.is_cuda:
             raise RuntimeError("aaclip ops need device (HIP) tensors; there is no CPU path")
+        if cur is None:
+            cur = torch.cuda.current_device()
+        if t.device.index != cur:
+            raise RuntimeError(f"aaclip op operand on {t.device} but the current device is cuda:{cur}; "
+                               "wrap the call in torch.cuda.device(...)")
 
 
 def _rowmajor(t: torch.Tensor, name: str):
@@ -350,6 +362,20 @@ def patch_scores(levels, T, out, *, normalize=True, mode=0, group=0):
     return out
 
 
+def patch_logits(f, T, out, *, group):
+    """Train-branch logits for any anchor count: out [B, n_anchor, group] = 100 * f . T."""
+    _dev(f, T, out)
+    _rowmajor(f, "f")
+    rows, C = f.shape
+    n = T.shape[1] if T.dim() == 2 else 0
+    if T.dim() != 2 or T.shape[0] != C or T.dtype != torch.float32 or not T.is_contiguous():
+        raise ValueError("T must be contiguous fp32 [C, n_anchor]")
+    if out.numel() < rows * n or out.dtype != torch.float32 or not out.is_contiguous() or group <= 0 or rows % group:
+        raise ValueError("patch_logits output / group mismatch")
+    call("aaclip_patch_logits", dtag(f), _ptr(f), f.stride(0), _ptr(T), n, rows, C, group, _ptr(out), _stream())
+    return out
+
+
 def blur_upsample(grid, out, *, ksize, sigma, softmax=False):
     _dev(grid, out)
     B, C, g, g2 = grid.shape
@@ -401,6 +427,11 @@ def metrics_eval(pixel_preds: torch.Tensor, pixel_label: torch.Tensor, image_pre
     il = (image_label.reshape(-1) != 0).to(torch.uint8).contiguous()
     if ip.numel() != N or il.numel() != N:
         raise ValueError("image_preds / image_label must have one entry per image")
+    with torch.cuda.device(preds.device):
+        return _metrics_eval_dev(preds, lab, ip, il, N, pix, medical)
+
+
+def _metrics_eval_dev(preds, lab, ip, il, N, pix, medical):
     _dev(preds, lab, ip, il)
     need = ctypes.c_size_t(0)
     call("aaclip_metrics_workspace", N * pix, N, ctypes.byref(need))

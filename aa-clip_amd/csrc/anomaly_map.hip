@@ -7,9 +7,9 @@
 // test score  sum_l (100 f^.t1 + 1 - 100 f^.t0) / 2  (the level sum is moved
 // ahead of blur+upsample, which are linear), or the two train logits.
 // Stage 2 — blur_upsample: one block per (image, band of output rows) stages
-// the tiny g x g score grid in LDS, applies the separable reflect-border
-// Gaussian (kornia 0.6.9 semantics) and writes the bilinear (align_corners)
-// upsample with 16-byte coalesced stores.
+// the grid rows the band needs in LDS, applies the separable reflect-border
+// Gaussian (kornia 0.6.9 semantics) to them and writes the bilinear
+// (align_corners) upsample with coalesced stores (any output size).
 #include <math.h>
 
 #include "common.h"
@@ -88,6 +88,41 @@ __global__ __launch_bounds__(256) void patch_scores_kernel(int in_dtype, LevelPt
   if (mode == 0 && lane == 0) out[row] = acc;
 }
 
+// Train-branch logits for any number of anchors (forward_utils.py:199-202 with
+// C anchors): out[b, a, p] = 100 * f[b*group + p] . T[:, a], channel-major so it
+// feeds blur_upsample directly. One wave per patch row, anchors in sequence.
+__global__ __launch_bounds__(256) void patch_logits_kernel(int in_dtype, const void* f, int64_t ld,
+                                                           const float* T, int n_anchor, int rows,
+                                                           int group, float* out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float4_t v[3];
+  if (in_dtype == AACLIP_F32) {
+    const float* p = (const float*)f + (size_t)row * ld;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = *(const float4_t*)(p + 256 * c + 4 * lane);
+  } else {
+    const uint16_t* p = (const uint16_t*)f + (size_t)row * ld;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      uint2 r = *(const uint2*)(p + 256 * c + 4 * lane);
+      v[c] = float4_t{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
+                      __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u)};
+    }
+  }
+  const size_t base = (size_t)(row / group) * n_anchor * group + row % group;
+  for (int a = 0; a < n_anchor; ++a) {
+    float d = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d += v[c][j] * T[(size_t)(256 * c + 4 * lane + j) * n_anchor + a];
+    d = wave_sum(d);
+    if (lane == 0) out[base + (size_t)a * group] = 100.0f * d;
+  }
+}
+
 // Reflect index for F.pad(mode='reflect') (no edge repeat).
 __device__ __forceinline__ int reflect(int i, int n) {
   i = i < 0 ? -i : i;
@@ -98,75 +133,107 @@ struct Gauss {
   float w[16];
 };
 
-constexpr int kBand = 16;  // output rows per block
+constexpr int kBand = 8;  // output rows per block
+constexpr int kMaxC = 8;  // channels of the train branch (anchors), softmax over them
 
-// grid: [B, C, g, g]; out: [B, C, S, S]. One block per (b, band).
+// grid: [B, C, g, g]; out: [B, C, S, S]. One block (4 waves) per (b, band of kBand
+// output rows). A band's bilinear taps read at most a few source rows, so only the
+// grid rows those need are staged and blurred: rows r_lo..r_hi for the y pass, their
+// reflect-padded neighbourhood r_lo-r..r_hi+r for the x pass (a reflected index of
+// that range stays inside it). One wave per grid row (lane = column, g <= 64): no
+// integer division anywhere. Same arithmetic, same order as the whole-grid blur, so
+// the output is bit-identical to it. The upsample runs one wave per output row:
+// 16-B stores of 4 consecutive pixels when S % 4 == 0, dword stores otherwise
+// (518 px, the reference's default size).
 __global__ __launch_bounds__(256) void blur_upsample_kernel(const float* grid, float* out, int C,
                                                             int g, int S, int ksize, Gauss gw,
                                                             int softmax, float scale) {
+  // no FMA contraction: ATen rounds src = scale * dst before taking the lambdas
+  // (a fused scale * dst - i0 shifts them by up to an ulp of src, ~1e-5 in the map)
+#pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int gg = g * g;
-  float* src = smem;           // C * gg (raw, then blurred)
-  float* tmp = smem + C * gg;  // C * gg
-  for (int i = threadIdx.x; i < C * gg; i += 256) src[i] = grid[(size_t)b * C * gg + i];
-  __syncthreads();
-  if (ksize > 0) {
-    const int r = ksize / 2;  // (k-1)//2 left pad == k//2 for odd k
-    for (int i = threadIdx.x; i < C * gg; i += 256) {  // x pass
-      const int c = i / gg, h = (i % gg) / g, w = i % g;
-      const float* row = src + c * gg + h * g;
-      float acc = 0.f;
-      for (int t = 0; t < ksize; ++t) acc += gw.w[t] * row[reflect(w + t - r, g)];
-      tmp[i] = acc;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < C * gg; i += 256) {  // y pass
-      const int c = i / gg, h = (i % gg) / g, w = i % g;
-      const float* col = tmp + c * gg + w;
-      float acc = 0.f;
-      for (int t = 0; t < ksize; ++t) acc += gw.w[t] * col[reflect(h + t - r, g) * g];
-      src[i] = acc;
-    }
-    __syncthreads();
-  }
+  float* src = smem;           // C * gg (raw, then blurred rows r_lo..r_hi)
+  float* tmp = smem + C * gg;  // C * gg (x-blurred rows)
   const int y0 = blockIdx.x * kBand;
   const int y1 = min(y0 + kBand, S);
-  const int groups = S / 4;  // S % 4 == 0 checked on the host
-  for (int idx = threadIdx.x; idx < (y1 - y0) * groups; idx += 256) {
-    const int y = y0 + idx / groups;
-    const int xq = (idx % groups) * 4;
+  const int r_lo = (int)(scale * (float)y0);
+  const int r_hi = min((int)(scale * (float)(y1 - 1)) + 1, g - 1);
+  const int r = ksize / 2;  // (k-1)//2 left pad == k//2 for odd k
+  const int x_lo = ksize > 0 ? max(0, r_lo - r) : r_lo;
+  const int x_hi = ksize > 0 ? min(g - 1, r_hi + r) : r_hi;
+  for (int c = 0; c < C; ++c)
+    for (int h = x_lo + wid; h <= x_hi; h += 4)
+      if (lane < g) src[c * gg + h * g + lane] = grid[((size_t)b * C + c) * gg + h * g + lane];
+  __syncthreads();
+  if (ksize > 0) {
+    for (int c = 0; c < C; ++c)  // x pass
+      for (int h = x_lo + wid; h <= x_hi; h += 4)
+        if (lane < g) {
+          const float* row = src + c * gg + h * g;
+          float acc = 0.f;
+          for (int t = 0; t < ksize; ++t) acc += gw.w[t] * row[reflect(lane + t - r, g)];
+          tmp[c * gg + h * g + lane] = acc;
+        }
+    __syncthreads();
+    for (int c = 0; c < C; ++c)  // y pass
+      for (int h = r_lo + wid; h <= r_hi; h += 4)
+        if (lane < g) {
+          const float* col = tmp + c * gg + lane;
+          float acc = 0.f;
+          for (int t = 0; t < ksize; ++t) acc += gw.w[t] * col[reflect(h + t - r, g) * g];
+          src[c * gg + h * g + lane] = acc;
+        }
+    __syncthreads();
+  }
+  const bool vec4 = (S & 3) == 0;
+  for (int y = y0 + wid; y < y1; y += 4) {
     // ATen upsample_bilinear2d, align_corners=True: src = scale * dst (fp32)
     const float sy = scale * (float)y;
     const int iy0 = (int)sy;
     const int iy1 = iy0 + (iy0 < g - 1 ? 1 : 0);
     const float hy1 = fminf(fmaxf(sy - (float)iy0, 0.f), 1.f), hy0 = 1.0f - hy1;
-    float v[2][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float sx = scale * (float)(xq + j);
-      const int ix0 = (int)sx;
-      const int ix1 = ix0 + (ix0 < g - 1 ? 1 : 0);
-      const float wx1 = fminf(fmaxf(sx - (float)ix0, 0.f), 1.f), wx0 = 1.0f - wx1;
-      for (int c = 0; c < C; ++c) {
-        const float* s = src + c * gg;
-        v[c][j] = hy0 * (wx0 * s[iy0 * g + ix0] + wx1 * s[iy0 * g + ix1]) +
-                  hy1 * (wx0 * s[iy1 * g + ix0] + wx1 * s[iy1 * g + ix1]);
-      }
-    }
-    if (softmax && C == 2) {
+    const int step = vec4 ? 256 : 64;
+    for (int x0 = (vec4 ? 4 : 1) * lane; x0 < S; x0 += step) {
+      float v[kMaxC][4];
+      const int nx = vec4 ? 4 : 1;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float m = fmaxf(v[0][j], v[1][j]);
-        const float e0 = expf(v[0][j] - m), e1 = expf(v[1][j] - m);
-        const float inv = 1.0f / (e0 + e1);
-        v[0][j] = e0 * inv;
-        v[1][j] = e1 * inv;
+        if (j >= nx) break;
+        const float sx = scale * (float)(x0 + j);
+        const int ix0 = (int)sx;
+        const int ix1 = ix0 + (ix0 < g - 1 ? 1 : 0);
+        const float wx1 = fminf(fmaxf(sx - (float)ix0, 0.f), 1.f), wx0 = 1.0f - wx1;
+        for (int c = 0; c < C; ++c) {
+          const float* s = src + c * gg;
+          v[c][j] = hy0 * (wx0 * s[iy0 * g + ix0] + wx1 * s[iy0 * g + ix1]) +
+                    hy1 * (wx0 * s[iy1 * g + ix0] + wx1 * s[iy1 * g + ix1]);
+        }
       }
-    }
-    for (int c = 0; c < C; ++c) {
-      float* o = out + (((size_t)b * C + c) * S + y) * S + xq;
-      *(float4_t*)o = float4_t{v[c][0], v[c][1], v[c][2], v[c][3]};
+      if (softmax && C > 1) {  // torch.softmax over the channel dim (forward_utils.py:214-215)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (j >= nx) break;
+          float m = v[0][j];
+          for (int c = 1; c < C; ++c) m = fmaxf(m, v[c][j]);
+          float sum = 0.f;
+          for (int c = 0; c < C; ++c) {
+            v[c][j] = expf(v[c][j] - m);
+            sum += v[c][j];
+          }
+          const float inv = 1.0f / sum;
+          for (int c = 0; c < C; ++c) v[c][j] *= inv;
+        }
+      }
+      for (int c = 0; c < C; ++c) {
+        float* o = out + (((size_t)b * C + c) * S + y) * S + x0;
+        if (vec4)
+          *(float4_t*)o = float4_t{v[c][0], v[c][1], v[c][2], v[c][3]};
+        else
+          *o = v[c][0];
+      }
     }
   }
 }
@@ -273,16 +340,31 @@ extern "C" int aaclip_patch_scores(int in_dtype, const void* const* levels, int 
   return AACLIP_OK;
 }
 
+extern "C" int aaclip_patch_logits(int in_dtype, const void* f, int64_t ld, const float* T, int n_anchor,
+                                   int rows, int channels, int group, float* out, void* stream) {
+  AACLIP_REQUIRE(in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16);
+  AACLIP_REQUIRE(f && T && out && rows >= 0 && channels == 768 && ld >= channels && ld % 4 == 0);
+  AACLIP_REQUIRE(n_anchor >= 1 && n_anchor <= 64 && group > 0 && rows % group == 0);
+  if (rows == 0) return AACLIP_OK;
+  patch_logits_kernel<<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(in_dtype, f, ld, T, n_anchor, rows,
+                                                                          group, out);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
 extern "C" int aaclip_blur_upsample(const float* grid, float* out, int batch, int channels, int g,
                                     int out_size, int ksize, float sigma, int softmax,
                                     void* stream) {
-  AACLIP_REQUIRE(grid && out && batch > 0 && (channels == 1 || channels == 2));
-  AACLIP_REQUIRE(g >= 2 && g <= 64 && out_size >= 2 && out_size % 4 == 0);
+  AACLIP_REQUIRE(grid && out && batch > 0 && channels >= 1 && channels <= kMaxC);
+  AACLIP_REQUIRE(g >= 2 && g <= 64 && out_size >= 2);
   AACLIP_REQUIRE(ksize >= 0 && ksize <= 15 && (ksize == 0 || (ksize % 2 == 1 && ksize / 2 < g)));
-  AACLIP_REQUIRE(!softmax || channels == 2);
   const Gauss gw = ksize > 0 ? gaussian_weights(ksize, sigma) : Gauss{};
   const float scale = (float)(g - 1) / (float)(out_size - 1);
-  const size_t lds = (size_t)2 * channels * g * g * sizeof(float);
+  const size_t lds = (size_t)(ksize > 0 ? 2 : 1) * channels * g * g * sizeof(float);
+  AACLIP_REQUIRE(lds <= 160 * 1024);
+  static unsigned attr_dev = 0;
+  if (lds > 64 * 1024 && !lds_attr_once((const void*)blur_upsample_kernel, 160 * 1024, attr_dev))
+    return AACLIP_ERR_LAUNCH;
   dim3 grd(ceil_div(out_size, kBand), batch);
   blur_upsample_kernel<<<grd, 256, lds, (hipStream_t)stream>>>(grid, out, channels, g, out_size,
                                                                ksize, gw, softmax, scale);

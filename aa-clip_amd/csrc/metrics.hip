@@ -266,9 +266,12 @@ int plan(int64_t n, int n_img, Layout& L) {
     o += align_up(bytes);
     return at;
   };
-  L.keys_a = take(8 * (size_t)n);
+  // keys_a (8 B per pixel) is reused, once sorted into keys_b, for two 4-B arrays
+  // (labels, group starts) at 256-B aligned offsets: size it for both aligned halves
+  // (8n alone is too small when 4n is not a multiple of 256, e.g. 4 maps of 518^2)
+  L.keys_a = take(2 * align_up(4 * (size_t)n));
   L.keys_b = take(8 * (size_t)n);
-  L.lbl = L.keys_a;                         // keys_a is free once sorted into keys_b
+  L.lbl = L.keys_a;
   L.gst = L.keys_a + align_up(4 * (size_t)n);
   L.P = take(4 * (size_t)n);
   L.A = take(4 * (size_t)n);
@@ -281,7 +284,6 @@ int plan(int64_t n, int n_img, Layout& L) {
   L.temp_bytes = std::max(sort_b, std::max(scan_b, max_b));
   L.temp = take(L.temp_bytes);
   L.total = o;
-  if (L.gst + 4 * (size_t)n > L.keys_a + align_up(8 * (size_t)n)) return AACLIP_ERR_ARG;
   return AACLIP_OK;
 }
 

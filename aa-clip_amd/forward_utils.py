@@ -90,8 +90,6 @@ def calculate_similarity_map(patch_features, epoch_text_feature, img_size, test=
     Cn = epoch_text_feature.shape[1]
     if test:
         assert Cn == 2
-    elif Cn != 2:
-        raise NotImplementedError("only the 2-anchor (normal, abnormal) form is on the path")
     f = patch_features.reshape(B * L, C)
     if f.dtype not in (torch.float32, torch.bfloat16):
         f = f.float()
@@ -104,10 +102,13 @@ def calculate_similarity_map(patch_features, epoch_text_feature, img_size, test=
         k, s = _blur_for(domain)
         out = torch.empty(B, 1, img_size, img_size, device=dev, dtype=torch.float32)
         return ops.blur_upsample(grid, out, ksize=k, sigma=s)
-    grid = torch.empty(B, 2, H, H, device=dev, dtype=torch.float32)
-    ops.patch_scores([f], T, grid, normalize=False, mode=1, group=L)
-    out = torch.empty(B, 2, img_size, img_size, device=dev, dtype=torch.float32)
-    return ops.blur_upsample(grid, out, ksize=0, sigma=0.0, softmax=True)
+    grid = torch.empty(B, Cn, H, H, device=dev, dtype=torch.float32)
+    if Cn == 2:
+        ops.patch_scores([f], T, grid, normalize=False, mode=1, group=L)
+    else:  # any anchor count (reference forward_utils.py:199-215 handles every C)
+        ops.patch_logits(f, T, grid, group=L)
+    out = torch.empty(B, Cn, img_size, img_size, device=dev, dtype=torch.float32)
+    return ops.blur_upsample(grid, out, ksize=0, sigma=0.0, softmax=Cn > 1)
 
 
 def anomaly_map_multilevel(patch_features, epoch_text_feature, img_size, domain="Industrial", normalize=False):

@@ -4,13 +4,18 @@ same flow, same outputs), running AdaptedCLIP on the MI355X kernels.
     python test.py --dataset MVTec --img_size 336 --save_path ckpt/...     (needs weights + data)
     python test.py --dataset synthetic --allow_random_init --img_size 336  (C1: no files needed)
     python test.py --dataset synthetic_mvtec --allow_random_init --img_size 336  (C4's 15-class flow)
+    torchrun --nproc-per-node 8 test.py ...   (C3-style: each class's images sharded over 8 GPUs)
 
 Differences from the reference, all on the host side:
   * the per-batch loop calls the fused AdaptedCLIP.predict (map + score in one
     device pass) and keeps results on the device (the reference syncs twice per
     batch, test.py:85,93); metrics_eval ranks the class's pixels on the device;
   * checkpoints load with torch.load(weights_only=True);
-  * --allow_random_init / --dataset synthetic run without the OpenAI weights.
+  * --allow_random_init / --dataset synthetic run without the OpenAI weights;
+  * under torchrun (WORLD_SIZE > 1, one process per GPU) every class's test set is
+    sharded by image (aaclip.parallel.shard_range), each rank predicts its shard and
+    the maps / scores / masks / labels are all-gathered (RCCL) before metrics_eval,
+    so every rank computes the same table; rank 0 prints and logs it.
 """
 from __future__ import annotations
 
@@ -42,7 +47,12 @@ def _device_batch(input_data, prep, device):
     return run(prep.images, input_data["image_u8"]), run(prep.masks, input_data["mask_u8"])
 
 
-def get_predictions(model, class_text_embeddings, test_loader, device, img_size, dataset="MVTec", prep=None):
+def get_predictions(model, class_text_embeddings, test_loader, device, img_size, dataset="MVTec", prep=None,
+                    n_total=None):
+    """test.py:53-99. With n_total (sharded run: test_loader holds this rank's
+    shard_range slice of a class's n_total images) the per-image results of all
+    ranks are all-gathered in shard order, so the return value is the whole class's
+    on every rank."""
     masks, labels, preds, preds_image, file_names = [], [], [], [], []
     for input_data in test_loader:
         if prep is not None:
@@ -58,11 +68,21 @@ def get_predictions(model, class_text_embeddings, test_loader, device, img_size,
         preds.append(pmap.clone())
         preds_image.append(score.clone())
     # maps and scores stay on the device: metrics_eval ranks them there
-    return (np.concatenate(masks, axis=0), np.concatenate(labels, axis=0), torch.cat(preds), torch.cat(preds_image),
-            file_names)
+    masks, labels = np.concatenate(masks, axis=0), np.concatenate(labels, axis=0)
+    preds, preds_image = torch.cat(preds), torch.cat(preds_image)
+    if n_total is not None:
+        import torch.distributed as dist
+        from aaclip.parallel import gather_rows
+        masks = gather_rows(torch.from_numpy(masks).to(preds.device), n_total).cpu().numpy()
+        labels = gather_rows(torch.from_numpy(labels).to(preds.device), n_total).cpu().numpy()
+        preds, preds_image = gather_rows(preds, n_total), gather_rows(preds_image, n_total)
+        names = [None] * dist.get_world_size()
+        dist.all_gather_object(names, file_names)
+        file_names = [f for part in names for f in part]
+    return masks, labels, preds, preds_image, file_names
 
 
-def main(argv=None):
+def parse_args(argv=None):
     parser = argparse.ArgumentParser(description="Testing")
     parser.add_argument("--model_name", type=str, default="ViT-L-14-336", help="ViT-L-14-336")
     parser.add_argument("--img_size", type=int, default=518)
@@ -82,19 +102,40 @@ def main(argv=None):
     parser.add_argument("--allow_random_init", action="store_true",
                         help="run on random-init CLIP + adapters when no checkpoints exist")
     parser.add_argument("--synthetic_n", type=int, default=16)
-    parser.add_argument("--compute_dtype", type=str, default="bf16", choices=["bf16", "fp32", "fp8"])
+    parser.add_argument("--compute_dtype", type=str, default="fp16", choices=["bf16", "fp16", "fp32", "fp8"],
+                        help="visual tower MFMA dtype: fp16 (default; meets the map-parity contract at the bf16 "
+                             "rate), bf16, fp32 (fp32-MFMA parity mode) or fp8 (config C5)")
     parser.add_argument("--gpu_preprocess", action="store_true",
                         help="decode on the host, resize + normalise on the GPU (bit-exact with the Pillow path)")
-    args = parser.parse_args(argv)
+    return parser.parse_args(argv)
 
+
+def main(argv=None):
+    return run(parse_args(argv))[0]
+
+
+def run(args):
+    """main() body; returns (results DataFrame, context dict with the model, the text
+    anchors and every class's (masks, labels, preds, preds_image)) for callers/tests."""
     setup_seed(args.seed)
-    os.makedirs(args.save_path, exist_ok=True)
-    logger = logging.getLogger(__name__)
-    logging.basicConfig(filename=os.path.join(args.save_path, "test.log"), encoding="utf-8", level=logging.INFO)
-    logger.info("args: %s", vars(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
     if not torch.cuda.is_available():
         raise RuntimeError("the AA-CLIP MI355X build needs a GPU (no CPU path)")
-    device = torch.device("cuda:0")
+    if world > 1:  # one process per GPU (torchrun); image-sharded classes
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        if not dist.is_initialized():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cuda:0")
+    os.makedirs(args.save_path, exist_ok=True)
+    logger = logging.getLogger(__name__)
+    if rank == 0:
+        logging.basicConfig(filename=os.path.join(args.save_path, "test.log"), encoding="utf-8", level=logging.INFO)
+    logger.info("args: %s", vars(args))
 
     clip_model = create_model(model_name=args.model_name, img_size=args.img_size, device=device,
                               pretrained=None if args.allow_random_init else "openai",
@@ -104,7 +145,7 @@ def main(argv=None):
     model = AdaptedCLIP(clip_model=clip_model, text_adapt_weight=args.text_adapt_weight,
                         image_adapt_weight=args.image_adapt_weight, text_adapt_until=args.text_adapt_until,
                         image_adapt_until=args.image_adapt_until, relu=args.relu,
-                        compute_dtype={"fp32": torch.float32, "fp8": torch.float8_e4m3fn}.get(
+                        compute_dtype={"fp32": torch.float32, "fp8": torch.float8_e4m3fn, "fp16": torch.float16}.get(
                             args.compute_dtype, torch.bfloat16)).to(device)
     model.eval()
 
@@ -142,25 +183,34 @@ def main(argv=None):
         with torch.no_grad():
             text_embeddings = get_adapted_text_embedding(model if adapt_text else clip_model, args.dataset, device)
         df = DataFrame(columns=["class name", "pixel AUC", "pixel AP", "image AUC", "image AP"])
+        ctx = {"model": model, "text_embeddings": text_embeddings, "classes": {}}
         for class_name, image_dataset in image_datasets.items():
             workers = 0 if synthetic else 4
             from dataset import collate_raw
+            n_total = None
+            if world > 1:
+                from aaclip.parallel import shard_range
+                n_total = len(image_dataset)
+                a, b = shard_range(n_total, rank, world)
+                image_dataset = torch.utils.data.Subset(image_dataset, range(a, b))
             loader = torch.utils.data.DataLoader(image_dataset, batch_size=args.batch_size, shuffle=False,
                                                  num_workers=workers, pin_memory=True,
                                                  collate_fn=collate_raw if raw else None)
             with torch.no_grad():
                 masks, labels, preds, preds_image, file_names = get_predictions(
                     model=model, class_text_embeddings=text_embeddings[class_name], test_loader=loader,
-                    device=device, img_size=args.img_size, dataset=args.dataset, prep=prep)
-            if args.visualize:
+                    device=device, img_size=args.img_size, dataset=args.dataset, prep=prep, n_total=n_total)
+            if args.visualize and rank == 0:
                 visualize(masks, preds.cpu().numpy(), file_names, args.save_path, args.dataset, class_name=class_name)
             result = metrics_eval(masks, labels, preds, preds_image, class_name, domain=DOMAINS[args.dataset])
+            ctx["classes"][class_name] = (masks, labels, preds, preds_image)
             df.loc[len(df)] = Series(result)
         df.loc[len(df)] = df.drop(columns=["class name"]).mean()
         df.loc[len(df) - 1, "class name"] = "Average"
         logger.info("final results:\n%s", df.to_string(index=False, justify="center"))
-        print(df.to_string(index=False, justify="center"))
-    return df
+        if rank == 0:
+            print(df.to_string(index=False, justify="center"))
+    return df, ctx
 
 
 if __name__ == "__main__":

@@ -45,7 +45,8 @@ extern "C" {
 #define AACLIP_EPI_AUX_BF16 16 /* also store a 16-bit copy of the result: fp16 when
                                   in_dtype is AACLIP_F16, bf16 otherwise      */
 
-/* ABI version (bumped on any signature change; 2 = MX fp8 LayerNorm outputs) and the target. */
+/* ABI version (bumped on any signature change; 2 = MX fp8 LayerNorm outputs, 3 = fp16 dtype,
+ * aaclip_patch_logits, any-size blur_upsample) and the target. */
 int aaclip_abi_version(void);
 const char* aaclip_arch(void);
 
@@ -252,10 +253,20 @@ int aaclip_patch_scores(int in_dtype, const void* const* levels, int n_levels, i
                         int group, float* out, void* stream);
 
 /*
+ * Train-branch logits for any number of anchors: out[b, a, p] = 100 * f[b*group+p] . T[:, a]
+ * (no normalisation; channel-major [B, n_anchor, group], the grid blur_upsample takes).
+ * f: [rows, channels] fp32/bf16 (channels == 768), T: [channels, n_anchor] fp32,
+ * 1 <= n_anchor <= 64. Replaces: forward_utils.py:199-202 for C != 2.
+ */
+int aaclip_patch_logits(int in_dtype, const void* f, int64_t ld, const float* T, int n_anchor,
+                        int rows, int channels, int group, float* out, void* stream);
+
+/*
  * Gaussian blur (kornia 0.6.9 gaussian_blur2d, reflect border, separable;
  * skipped when ksize == 0) then bilinear upsample with align_corners=True
- * (F.interpolate), optional softmax over the channel dim (train branch).
- * grid: [batch, channels, g, g] fp32 -> out [batch, channels, S, S] fp32.
+ * (F.interpolate) to any out_size, optional softmax over the channel dim
+ * (train branch, any 1 <= channels <= 8; channels == 1 leaves the logits as they are).
+ * grid: [batch, channels, g, g] fp32 (g <= 64) -> out [batch, channels, S, S] fp32.
  * Replaces: forward_utils.py:208-215.
  */
 int aaclip_blur_upsample(const float* grid, float* out, int batch, int channels, int g,

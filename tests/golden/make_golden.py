@@ -18,6 +18,9 @@ every fixture here is "reference code on synthetic weights". Outputs:
                     adapter blend, similarity map incl. train branch, metrics_eval)
   golden_c5.npz     config-C5 shapes: 448 px (1025 tokens), 6 levels [4..24],
                     relu=True projections, Medical-domain map, B=1
+  golden_518.npz    the reference's default test size (test.py:111, results/test.log:1-3):
+                    518 px (37x37 grid, 1370 tokens), 4 levels, B=1, both domains
+                    (`python tests/golden/make_golden.py 518` regenerates only this file)
   ../../aa-clip_amd/model/prompt_tokens.json   token ids of every prompt the
                     reference can build (tokenizer.py:150-185 over
                     dataset/constants.py:78-148)
@@ -257,5 +260,31 @@ def main():
         print(fn, os.path.getsize(os.path.join(HERE, fn)))
 
 
+@torch.no_grad()
+def main_518():
+    """518 px: 37x37 patch grid (1369 patches + CLS = 1370 tokens), the size of every
+    published number; maps are not a multiple of 4 wide (518 % 4 = 2)."""
+    _, model, sd, img_ad, _ = build_reference(img_size=518)
+    import forward_utils as fu
+    text = np.load(os.path.join(HERE, "golden_text.npz"))
+    T = t(text["bottle_T_adapted"])
+    x = synth.images(SEED, 1, 518)
+    seg, det = model(t(x))
+    out = dict(image_sha=np.array(synth.state_checksum({"x": x})), clip_sha=np.array(synth.state_checksum(sd)),
+               T=text["bottle_T_adapted"],
+               grid_A=np.stack([(100.0 * (f @ T)).numpy() for f in seg], axis=1).astype(np.float32),
+               det=det.numpy(), score=((det @ T)[:, 1].numpy() + 1) / 2)
+    for dom in ("Industrial", "Medical"):
+        m = torch.cat([fu.calculate_similarity_map(f, T, 518, test=True, domain=dom) for f in seg], 1).sum(1).numpy()
+        out[f"map_{dom}_sub"] = m[:, ::7, ::7]      # every column residue mod 4 and 7
+        out[f"map_{dom}_rows"] = m[:, [0, 1, 258, 517], :]  # whole rows incl. the last columns
+    np.savez_compressed(os.path.join(HERE, "golden_518.npz"), **out)
+    print("golden_518.npz", os.path.getsize(os.path.join(HERE, "golden_518.npz")))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["518"]:
+        main_518()
+    else:
+        main()
+        main_518()

@@ -3,7 +3,7 @@ OpenAI state-dict layout (oracle/synth.py:write_openai_checkpoint) loaded by the
 reference create_model(..., pretrained='openai') (model/clip.py:84-142 ->
 model/openai.py:17-83 -> build_model_from_openai_state_dict + fp16 convert_weights,
 model/model.py:265-286, :311-368; resize_pos_embed bicubic+antialias, model.py:395-426)
-at 336 px (no resize) and 448 px (24 -> 32 grid). Records SHA-256 of the loaded fp32
+at 336 px (no resize), 448 px (24 -> 32 grid) and 518 px (24 -> 37, the reference's default). Records SHA-256 of the loaded fp32
 state dicts and the resized positional embedding's first rows.
 Build container only: PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_load_golden.py"""
 import json
@@ -35,7 +35,7 @@ def main():
         ck = os.path.join(d, "ViT-L-14-336px.pt")
         synth.write_openai_checkpoint(ck, 111)
         rclip._MODEL_CKPT_PATHS["ViT-L-14-336"] = ck
-        for size in (336, 448):
+        for size in (336, 448, 518):
             m = rclip.create_model("ViT-L-14-336", size, pretrained="openai")
             sd = m.state_dict()
             out[str(size)] = {"sha256": synth.torch_state_checksum(sd),

@@ -60,3 +60,74 @@ def test_gloo_world2_gather(n):
     for _, s, m in out:
         assert s == [i * 0.5 + 1.0 for i in range(n)]
         assert m == [float(i) for i in range(n)]
+
+
+class _StandIn:
+    """CPU stand-in for AdaptedCLIP.predict: per-image map and score that depend only
+    on that image (the property the image sharding relies on)."""
+
+    def predict(self, image, T, domain="Industrial", streams=1):
+        maps = image.mean(1) * T.sum()
+        return maps, maps.mean((1, 2)) + image[:, 0, 0, 0]
+
+
+def _sharded_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "aa-clip_amd"))
+    import test as harness
+    from aaclip.parallel import sharded_step
+    from dataset import get_dataset
+    model = _StandIn()
+    T = torch.full((4, 2), 0.5)
+    # bench step: this rank's shard_range slice of one global batch -> gathered scores
+    g = torch.Generator().manual_seed(111)
+    x_global = torch.randn(n, 3, 28, 28, generator=g)
+    a, b = shard_range(n, rank, world)
+    _, _, s_all, m_all = sharded_step(model.predict, x_global[a:b], T, n, gather_maps=True)
+    # harness: one class's dataset sharded by image, gathered before metrics
+    ds = get_dataset("synthetic", 28, None, -1, "test", synthetic_n=n)["bottle"]
+    sub = torch.utils.data.Subset(ds, range(*shard_range(n, rank, world)))
+    loader = torch.utils.data.DataLoader(sub, batch_size=3, shuffle=False)
+    masks, labels, preds, preds_image, names = harness.get_predictions(model, T, loader, torch.device("cpu"), 28,
+                                                                       dataset="synthetic", n_total=n)
+    q.put((rank, s_all.tolist(), m_all.sum().item(), masks.sum(), labels.tolist(), preds.sum().item(),
+           preds_image.tolist(), names))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [8, 7])
+def test_gloo_world2_sharded_step_and_harness(n):
+    """The bench's data-parallel step (aaclip.parallel.sharded_step) and the harness's
+    sharded get_predictions on 2 gloo ranks with a CPU stand-in predictor: every rank
+    ends with exactly the unsharded run's scores, maps, masks, labels and file names."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "aa-clip_amd"))
+    import test as harness
+    from dataset import get_dataset
+    model = _StandIn()
+    T = torch.full((4, 2), 0.5)
+    g = torch.Generator().manual_seed(111)
+    x_global = torch.randn(n, 3, 28, 28, generator=g)
+    ref_maps, ref_scores = model.predict(x_global, T)
+    ds = get_dataset("synthetic", 28, None, -1, "test", synthetic_n=n)["bottle"]
+    ref = harness.get_predictions(model, T, torch.utils.data.DataLoader(ds, batch_size=3, shuffle=False),
+                                  torch.device("cpu"), 28, dataset="synthetic")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, s_all, m_sum, mk_sum, labels, p_sum, pi, names in out:
+        assert s_all == ref_scores.tolist()
+        assert m_sum == ref_maps.sum().item()
+        assert mk_sum == ref[0].sum() and labels == ref[1].tolist()
+        assert p_sum == ref[2].sum().item() and pi == ref[3].tolist() and names == ref[4]

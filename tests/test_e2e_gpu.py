@@ -201,3 +201,37 @@ def test_text_encode_sequence_invariance(dev, golden, weights, dtype):
     for i in (0, 4, tok.shape[0] - 1):
         assert torch.equal(eng.encode(tok[i:i + 1]), full[i:i + 1]), i
     assert torch.equal(eng.encode(tok[3:6]), full[3:6])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+def test_518_default_size_parity(dev, dtype):
+    """518 px (the reference's default, test.py:111): 37x37 grid, 1370-token attention
+    (key tail of 26 in a masked tile), 518-wide maps, vs the reference's golden.
+    fp32 and fp16 meet the north_star contract on every sampled pixel; bf16 is held to
+    the looser bound its 8-bit operands allow."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_518.npz"))
+    sd = synth.clip_state_dict(111, img_size=518)
+    ia, _ = synth.adapter_state_dicts(111)
+    vp = {k: torch.from_numpy(v).to(dev) for k, v in sd.items() if k.startswith("visual.")}
+    eng = VisualEngine(vp, {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}, dtype=dtype)
+    x = torch.from_numpy(synth.images(111, 1, 518)).to(dev)
+    T = torch.from_numpy(g["T"]).to(dev)
+    for dom in ("Industrial", "Medical"):
+        maps, score = eng.predict(x, T, dom)
+        m = maps.cpu().numpy()
+        for got, ref in ((m[:, ::7, ::7], g[f"map_{dom}_sub"]), (m[:, [0, 1, 258, 517], :], g[f"map_{dom}_rows"])):
+            err = np.abs(got - ref)
+            print(dtype, dom, "518 map max abs err", err.max())
+            if dtype == torch.bfloat16:
+                assert (err <= 3e-3 + 1.5e-2 * np.abs(ref)).all()
+            else:
+                assert (err <= 1e-3 + 1e-2 * np.abs(ref)).all()
+        np.testing.assert_allclose(score.cpu().numpy(), g["score"], atol=1e-4 if dtype != torch.bfloat16 else 1e-3)
+    if dtype == torch.float32:
+        seg, det = eng.forward(x)
+        grid = np.stack([(100.0 * (f @ T)).cpu().numpy() for f in seg], axis=1)
+        ref = g["grid_A"]
+        sure = np.abs(ref[..., 1] - ref[..., 0]) > 1e-3
+        assert int((grid.argmax(-1) != ref.argmax(-1))[sure].sum()) == 0
+        np.testing.assert_allclose(grid, ref, atol=5e-3)

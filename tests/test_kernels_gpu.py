@@ -399,3 +399,35 @@ def test_image_score(dev):
     ref_det = R.l2_normalize(d).mean(1)
     np.testing.assert_allclose(det.cpu().numpy(), ref_det, atol=1e-6, rtol=1e-5)
     np.testing.assert_allclose(score.cpu().numpy(), R.image_score(ref_det, T), atol=1e-6)
+
+
+@pytest.mark.parametrize("g,S", [(37, 518), (37, 517), (24, 336), (24, 41), (8, 130), (32, 448), (5, 2), (64, 900)])
+@pytest.mark.parametrize("ksize,sigma", [(7, 1.0), (9, 1.5), (0, 0.0)])
+def test_blur_upsample_any_size(dev, g, S, ksize, sigma):
+    """Band-local blur + bilinear upsample at any output size (518 = the reference's
+    default, 518 % 4 = 2: dword-store path) vs the numpy restatement of kornia's
+    gaussian_blur2d + ATen's align_corners upsample."""
+    if ksize // 2 >= g:
+        pytest.skip("kernel wider than the grid")
+    rng = np.random.default_rng(g * 1000 + S + ksize)
+    B = 3
+    grid = rng.standard_normal((B, 1, g, g)).astype(np.float32)
+    out = torch.full((B, 1, S, S), float("nan"), device=dev)
+    ops.blur_upsample(torch.from_numpy(grid).to(dev), out, ksize=ksize, sigma=sigma)
+    ref = R.gaussian_blur2d(grid, ksize, sigma) if ksize else grid
+    ref = R.upsample_bilinear_ac(ref, S)
+    got = out.cpu().numpy()
+    assert not np.isnan(got).any()
+    np.testing.assert_allclose(got, ref, atol=2e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("S", [518, 40, 337])
+def test_blur_upsample_train_softmax_any_size(dev, S):
+    """Train branch (2 channels, no blur, softmax over channels) at odd output sizes."""
+    rng = np.random.default_rng(S)
+    g = 37 if S == 518 else 8
+    grid = (rng.standard_normal((2, 2, g, g)) * 3).astype(np.float32)
+    out = torch.empty(2, 2, S, S, device=dev)
+    ops.blur_upsample(torch.from_numpy(grid).to(dev), out, ksize=0, sigma=0.0, softmax=True)
+    ref = R.softmax(R.upsample_bilinear_ac(grid, S), axis=1)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-6, rtol=1e-5)

@@ -109,3 +109,15 @@ def test_forward_utils_metrics_device_tensors(dev):
     assert r["class name"] == "cls"
     assert [r[k] for k in ("pixel AUC", "pixel AP", "image AUC", "image AP")] == \
         pytest.approx([round(v, 4) * 100 for v in want], abs=1e-9)
+
+
+@pytest.mark.parametrize("N,S", [(4, 518), (3, 37), (5, 41), (1, 17)])
+def test_metrics_ragged_pixel_counts(dev, N, S):
+    """Pixel counts whose 4-byte arrays are not 256-B multiples (4 maps of 518^2: the
+    reference's default size) — the workspace carve-up must still fit."""
+    masks, labels, pp, ip = _case(N * S, N, S)
+    if N == 1:
+        labels[0] = 1
+    got = _dev_metrics(dev, masks, labels, pp, ip, "Industrial")
+    want = _sk(masks, labels, pp.copy(), ip.copy(), "Industrial")
+    assert np.allclose(got, want, rtol=0, atol=1e-9), (got, want)

@@ -3,7 +3,8 @@ OpenAI-layout checkpoint (oracle/synth.py:write_openai_checkpoint) through
 create_model(..., pretrained='openai') must give a bit-identical fp32 state dict to
 the reference's (tests/golden/golden_load.json, tests/golden/make_load_golden.py):
 fp16 effective-weight rounding of the OpenAI-cast tensors, dropped metadata entries,
-and the bicubic+antialias positional-embedding resize 24x24 -> 32x32 at 448 px.
+and the bicubic+antialias positional-embedding resize 24x24 -> 32x32 at 448 px and
+-> 37x37 at 518 px (the reference's default size).
 CPU only (~850 MB temporary checkpoint)."""
 import json
 import os
@@ -22,7 +23,7 @@ def checkpoint(tmp_path_factory):
     return path
 
 
-@pytest.mark.parametrize("size", [336, 448])
+@pytest.mark.parametrize("size", [336, 448, 518])
 def test_openai_checkpoint_load_matches_reference(checkpoint, size, monkeypatch):
     import model.clip as clip
     golden = json.load(open(os.path.join(HERE, "golden", "golden_load.json")))[str(size)]
