@@ -387,11 +387,14 @@ def blur_upsample(grid, out, *, ksize, sigma, softmax=False):
 
 
 def anomaly_map(levels, T, out, grid_ws, *, g, ksize, sigma, normalize=True):
+    """Test-branch map of all levels: patch_scores into grid_ws (>= B*g*g fp32), then blur_upsample."""
     _dev(*levels, T, out, grid_ws)
     B, S, S2 = out.shape
     rows, C = levels[0].shape
-    if rows != B * g * g or S != S2 or grid_ws.numel() < rows:
-        raise ValueError("anomaly_map shape mismatch")
+    if rows != B * g * g or S != S2 or grid_ws.numel() < rows or grid_ws.dtype != torch.float32:
+        raise ValueError("anomaly_map shape mismatch (grid_ws: fp32 >= [B*g*g])")
+    if not out.is_contiguous():
+        raise ValueError("anomaly_map output must be contiguous")
     for t in levels:
         if t.shape != (rows, C) or t.stride(0) != levels[0].stride(0) or t.dtype != levels[0].dtype:
             raise ValueError("levels must share shape, dtype and stride")

@@ -6,7 +6,7 @@
 // computes ||f||, f.t0, f.t1 with wave shuffles, and emits the level-summed
 // test score  sum_l (100 f^.t1 + 1 - 100 f^.t0) / 2  (the level sum is moved
 // ahead of blur+upsample, which are linear), or the two train logits.
-// Stage 2 — blur_upsample: one block per (image, band of output rows) stages
+// Stage 2 — blur_upsample: one wave per (image, band of output rows) stages
 // the grid rows the band needs in LDS, applies the separable reflect-border
 // Gaussian (kornia 0.6.9 semantics) to them and writes the bilinear
 // (align_corners) upsample with coalesced stores (any output size).
@@ -21,15 +21,8 @@ struct LevelPtrs {
   const void* p[kMaxLevels];
 };
 
-__global__ __launch_bounds__(256) void patch_scores_kernel(int in_dtype, LevelPtrs lv, int nl,
-                                                           int64_t ld, const float* T, int rows,
-                                                           int normalize, int mode, int group,
-                                                           float* out) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  // anchors at this lane's 12 channels (C = 768 = 3 x 256)
-  float4_t t0[3], t1[3];
+// The lane's 12 anchor channels (C = 768 = 3 x 256): t0 / t1 = normal / abnormal.
+__device__ __forceinline__ void load_anchors(const float* T, float4_t (&t0)[3], float4_t (&t1)[3], int lane) {
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float* tp = T + 2 * (256 * c + 4 * lane);
@@ -37,17 +30,32 @@ __global__ __launch_bounds__(256) void patch_scores_kernel(int in_dtype, LevelPt
     t0[c] = float4_t{a[0], a[2], b[0], b[2]};
     t1[c] = float4_t{a[1], a[3], b[1], b[3]};
   }
-  // issue every level's loads before reducing (memory-level parallelism)
+}
+
+// One patch row through every level (one wave): loads of all levels issued before
+// the reductions (memory-level parallelism), then ||f||, f.t0, f.t1 per level.
+// mode 0 returns sum_l (A1 + 1 - A0) / 2 (every lane); mode 1 (one level) writes
+// the two logits [b, 2, group] from lane 0.
+// F32IN: fp32 features (compile time, so every level's loads issue back to back
+// with no per-level dtype branch and its vmcnt(0) join), else bf16.
+template <bool F32IN>
+__device__ __forceinline__ float patch_row_score(LevelPtrs lv, int nl, int64_t ld, size_t row,
+                                                 const float4_t (&t0)[3], const float4_t (&t1)[3], int normalize,
+                                                 int mode, int group, float* out, int lane) {
+  // explicit FMAs and no other contraction: the same bits in every kernel that
+  // inlines this (patch_scores_kernel, anomaly_map_kernel), whatever the compiler
+  // would fuse in each context
+#pragma clang fp contract(off)
   float4_t f[kMaxLevels][3];
 #pragma unroll
   for (int l = 0; l < kMaxLevels; ++l) {
     if (l < nl) {
-      if (in_dtype == AACLIP_F32) {
-        const float* p = (const float*)lv.p[l] + (size_t)row * ld;
+      if constexpr (F32IN) {
+        const float* p = (const float*)lv.p[l] + row * ld;
 #pragma unroll
         for (int c = 0; c < 3; ++c) f[l][c] = *(const float4_t*)(p + 256 * c + 4 * lane);
       } else {
-        const uint16_t* p = (const uint16_t*)lv.p[l] + (size_t)row * ld;
+        const uint16_t* p = (const uint16_t*)lv.p[l] + row * ld;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           uint2 r = *(const uint2*)(p + 256 * c + 4 * lane);
@@ -67,9 +75,9 @@ __global__ __launch_bounds__(256) void patch_scores_kernel(int in_dtype, LevelPt
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float v = f[l][c][j];
-          ss += v * v;
-          a0 += v * t0[c][j];
-          a1 += v * t1[c][j];
+          ss = fmaf(v, v, ss);
+          a0 = fmaf(v, t0[c][j], a0);
+          a1 = fmaf(v, t1[c][j], a1);
         }
       ss = wave_sum(ss);
       a0 = wave_sum(a0);
@@ -79,12 +87,26 @@ __global__ __launch_bounds__(256) void patch_scores_kernel(int in_dtype, LevelPt
       if (mode == 0) {
         acc += (A1 + 1.0f - A0) / 2.0f;
       } else if (lane == 0) {
-        const size_t base = (size_t)(row / group) * 2 * group + row % group;
+        const size_t base = (row / group) * 2 * group + row % group;
         out[base] = A0;
         out[base + group] = A1;
       }
     }
   }
+  return acc;
+}
+
+template <bool F32IN>
+__global__ __launch_bounds__(256) void patch_scores_kernel(LevelPtrs lv, int nl,
+                                                           int64_t ld, const float* T, int rows,
+                                                           int normalize, int mode, int group,
+                                                           float* out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float4_t t0[3], t1[3];
+  load_anchors(T, t0, t1, lane);
+  const float acc = patch_row_score<F32IN>(lv, nl, ld, (size_t)row, t0, t1, normalize, mode, group, out, lane);
   if (mode == 0 && lane == 0) out[row] = acc;
 }
 
@@ -133,30 +155,29 @@ struct Gauss {
   float w[16];
 };
 
-constexpr int kBand = 8;  // output rows per block
+constexpr int kBand = 8;  // output rows per wave (= per workgroup); 4 and 8 measured equal, 2 / 16 slower
 constexpr int kMaxC = 8;  // channels of the train branch (anchors), softmax over them
 
-// grid: [B, C, g, g]; out: [B, C, S, S]. One block (4 waves) per (b, band of kBand
-// output rows). A band's bilinear taps read at most a few source rows, so only the
-// grid rows those need are staged and blurred: rows r_lo..r_hi for the y pass, their
-// reflect-padded neighbourhood r_lo-r..r_hi+r for the x pass (a reflected index of
-// that range stays inside it). One wave per grid row (lane = column, g <= 64): no
-// integer division anywhere. Same arithmetic, same order as the whole-grid blur, so
-// the output is bit-identical to it. The upsample runs one wave per output row:
-// 16-B stores of 4 consecutive pixels when S % 4 == 0, dword stores otherwise
-// (518 px, the reference's default size).
-__global__ __launch_bounds__(256) void blur_upsample_kernel(const float* grid, float* out, int C,
-                                                            int g, int S, int ksize, Gauss gw,
-                                                            int softmax, float scale) {
-  // no FMA contraction: ATen rounds src = scale * dst before taking the lambdas
-  // (a fused scale * dst - i0 shifts them by up to an ulp of src, ~1e-5 in the map)
+// Stage 2: one WAVE per (image, band of kBand output rows) — no workgroup barriers
+// (a wave's LDS operations execute in order). The band's bilinear taps read source
+// rows r_lo..r_hi only, so the wave stages the raw rows those need (their reflect
+// neighbourhood x_lo..x_hi; a reflected index of that range stays inside it), x-blurs
+// them, y-blurs rows r_lo..r_hi, and writes the band: 16-B stores of 4 consecutive
+// pixels when S % 4 == 0, dwords otherwise (518 px, the reference's default).
+// kornia 0.6.9 gaussian_blur2d semantics (separable, reflect border, x then y) and
+// ATen's align_corners bilinear arithmetic (src = scale * dst rounded before the
+// lambdas: no FMA contraction). K = ksize at compile time for the domains' 7 and 9
+// (tap loads issued together), -1 = any ksize at run time, 0 = no blur.
+// LDS: C * (2 * xrows + brows) * g floats, sized by the host for the band.
+template <int C, int K>
+__global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, float* out, int g, int S,
+                                                           int ksize_rt, Gauss gw, int softmax, float scale,
+                                                           int xrows, int brows) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int ksize = K >= 0 ? K : ksize_rt;
+  const int lane = threadIdx.x;
   const int b = blockIdx.y;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int gg = g * g;
-  float* src = smem;           // C * gg (raw, then blurred rows r_lo..r_hi)
-  float* tmp = smem + C * gg;  // C * gg (x-blurred rows)
   const int y0 = blockIdx.x * kBand;
   const int y1 = min(y0 + kBand, S);
   const int r_lo = (int)(scale * (float)y0);
@@ -164,75 +185,142 @@ __global__ __launch_bounds__(256) void blur_upsample_kernel(const float* grid, f
   const int r = ksize / 2;  // (k-1)//2 left pad == k//2 for odd k
   const int x_lo = ksize > 0 ? max(0, r_lo - r) : r_lo;
   const int x_hi = ksize > 0 ? min(g - 1, r_hi + r) : r_hi;
-  for (int c = 0; c < C; ++c)
-    for (int h = x_lo + wid; h <= x_hi; h += 4)
-      if (lane < g) src[c * gg + h * g + lane] = grid[((size_t)b * C + c) * gg + h * g + lane];
-  __syncthreads();
-  if (ksize > 0) {
-    for (int c = 0; c < C; ++c)  // x pass
-      for (int h = x_lo + wid; h <= x_hi; h += 4)
-        if (lane < g) {
-          const float* row = src + c * gg + h * g;
-          float acc = 0.f;
-          for (int t = 0; t < ksize; ++t) acc += gw.w[t] * row[reflect(lane + t - r, g)];
-          tmp[c * gg + h * g + lane] = acc;
-        }
-    __syncthreads();
-    for (int c = 0; c < C; ++c)  // y pass
-      for (int h = r_lo + wid; h <= r_hi; h += 4)
-        if (lane < g) {
-          const float* col = tmp + c * gg + lane;
-          float acc = 0.f;
-          for (int t = 0; t < ksize; ++t) acc += gw.w[t] * col[reflect(h + t - r, g) * g];
-          src[c * gg + h * g + lane] = acc;
-        }
-    __syncthreads();
+  const int nx = x_hi - x_lo + 1, nb = r_hi - r_lo + 1;
+  float* raw = smem;                  // [C][xrows][g]: rows x_lo..
+  float* xbl = raw + C * xrows * g;   // [C][xrows][g]: x-blurred rows x_lo..
+  float* bl = xbl + C * xrows * g;    // [C][brows][g]: blurred rows r_lo..
+  if (lane < g) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      for (int h = 0; h < nx; ++h) raw[(c * xrows + h) * g + lane] = grid[(((size_t)b * C + c) * g + x_lo + h) * g + lane];
   }
-  const bool vec4 = (S & 3) == 0;
-  for (int y = y0 + wid; y < y1; y += 4) {
-    // ATen upsample_bilinear2d, align_corners=True: src = scale * dst (fp32)
-    const float sy = scale * (float)y;
-    const int iy0 = (int)sy;
-    const int iy1 = iy0 + (iy0 < g - 1 ? 1 : 0);
-    const float hy1 = fminf(fmaxf(sy - (float)iy0, 0.f), 1.f), hy0 = 1.0f - hy1;
-    const int step = vec4 ? 256 : 64;
-    for (int x0 = (vec4 ? 4 : 1) * lane; x0 < S; x0 += step) {
-      float v[kMaxC][4];
-      const int nx = vec4 ? 4 : 1;
+  __builtin_amdgcn_wave_barrier();
+  const float* src = raw;  // rows relative to x_lo (== r_lo without blur)
+  int sld = xrows;
+  if (ksize > 0) {
+    if (lane < g) {
+      int xi[16];  // reflected column of each tap (shared by every row)
+      const int kk = K > 0 ? K : ksize;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (j >= nx) break;
-        const float sx = scale * (float)(x0 + j);
-        const int ix0 = (int)sx;
-        const int ix1 = ix0 + (ix0 < g - 1 ? 1 : 0);
-        const float wx1 = fminf(fmaxf(sx - (float)ix0, 0.f), 1.f), wx0 = 1.0f - wx1;
-        for (int c = 0; c < C; ++c) {
-          const float* s = src + c * gg;
-          v[c][j] = hy0 * (wx0 * s[iy0 * g + ix0] + wx1 * s[iy0 * g + ix1]) +
-                    hy1 * (wx0 * s[iy1 * g + ix0] + wx1 * s[iy1 * g + ix1]);
+      for (int t = 0; t < (K > 0 ? K : 15); ++t)
+        if (t < kk) xi[t] = reflect(lane + t - r, g);
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        for (int h = 0; h < nx; ++h) {
+          const float* row = raw + (c * xrows + h) * g;
+          float acc = 0.f;
+#pragma unroll
+          for (int t = 0; t < (K > 0 ? K : 15); ++t)
+            if (t < kk) acc += gw.w[t] * row[xi[t]];
+          xbl[(c * xrows + h) * g + lane] = acc;
         }
-      }
-      if (softmax && C > 1) {  // torch.softmax over the channel dim (forward_utils.py:214-215)
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (j >= nx) break;
-          float m = v[0][j];
-          for (int c = 1; c < C; ++c) m = fmaxf(m, v[c][j]);
+      for (int c = 0; c < C; ++c)
+        for (int j = 0; j < nb; ++j) {
+          const int h = r_lo + j;
+          const float* col = xbl + c * xrows * g + lane;
+          float acc = 0.f;
+#pragma unroll
+          for (int t = 0; t < (K > 0 ? K : 15); ++t)
+            if (t < kk) acc += gw.w[t] * col[(reflect(h + t - r, g) - x_lo) * g];
+          bl[(c * brows + j) * g + lane] = acc;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    src = bl;
+    sld = brows;
+  }
+  // Upsample. Per lane 8 columns of a 512-column chunk (16-B path: 4 consecutive
+  // pixels at 4*lane + 256*it; dword path: lane + 64*it). The column taps (ix0, ix1,
+  // wx0, wx1) are computed once per chunk, and the horizontal blends
+  // H_j(x) = wx0 * s[j][ix0] + wx1 * s[j][ix1] once per source row j: every output row
+  // with iy0 = j reuses them (~15 rows per source row at 336 / 518 px), leaving
+  // hy0 * H_iy0 + hy1 * H_iy1 per pixel -- ATen's expression, same order, same bits.
+  const bool vec4 = (S & 3) == 0;
+  for (int cx = 0; cx < S; cx += 512) {
+    int o0[8], o1[8];
+    float w0[8], w1[8];
+    bool ok[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int x = cx + (vec4 ? 4 * lane + 256 * (p >> 2) + (p & 3) : lane + 64 * p);
+      ok[p] = x < S;
+      const float sx = scale * (float)x;
+      const int ix0 = (int)sx;
+      const int ix1 = ix0 + (ix0 < g - 1 ? 1 : 0);
+      w1[p] = fminf(fmaxf(sx - (float)ix0, 0.f), 1.f);
+      w0[p] = 1.0f - w1[p];
+      o0[p] = ok[p] ? ix0 : 0;
+      o1[p] = ok[p] ? ix1 : 0;
+    }
+    float H0[C][8], H1[C][8];
+    auto hblend = [&](int jrow, float (&H)[C][8]) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float* sr = src + (c * sld + jrow) * g;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) H[c][p] = w0[p] * sr[o0[p]] + w1[p] * sr[o1[p]];
+      }
+    };
+    int cur0 = -1, cur1 = -1;
+    for (int y = y0; y < y1; ++y) {
+      // ATen upsample_bilinear2d, align_corners=True: src = scale * dst (fp32)
+      const float sy = scale * (float)y;
+      const int iy0 = (int)sy;
+      const int iy1 = iy0 + (iy0 < g - 1 ? 1 : 0);
+      const float hy1 = fminf(fmaxf(sy - (float)iy0, 0.f), 1.f), hy0 = 1.0f - hy1;
+      if (iy0 != cur0) {
+        if (iy0 == cur1) {
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 8; ++p) H0[c][p] = H1[c][p];
+        } else {
+          hblend(iy0 - r_lo, H0);
+        }
+        cur0 = iy0;
+      }
+      if (iy1 != cur1) {
+        hblend(iy1 - r_lo, H1);
+        cur1 = iy1;
+      }
+      float v[C][8];
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) v[c][p] = hy0 * H0[c][p] + hy1 * H1[c][p];
+      if (C > 1 && softmax) {  // torch.softmax over the channel dim (forward_utils.py:214-215)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          float m = v[0][p];
+#pragma unroll
+          for (int c = 1; c < C; ++c) m = fmaxf(m, v[c][p]);
           float sum = 0.f;
+#pragma unroll
           for (int c = 0; c < C; ++c) {
-            v[c][j] = expf(v[c][j] - m);
-            sum += v[c][j];
+            v[c][p] = expf(v[c][p] - m);
+            sum += v[c][p];
           }
           const float inv = 1.0f / sum;
-          for (int c = 0; c < C; ++c) v[c][j] *= inv;
+#pragma unroll
+          for (int c = 0; c < C; ++c) v[c][p] *= inv;
         }
       }
+#pragma unroll
       for (int c = 0; c < C; ++c) {
-        float* o = out + (((size_t)b * C + c) * S + y) * S + x0;
-        if (vec4)
-          *(float4_t*)o = float4_t{v[c][0], v[c][1], v[c][2], v[c][3]};
-        else
-          *o = v[c][0];
+        float* orow = out + (((size_t)b * C + c) * S + y) * S + cx;
+        if (vec4) {
+#pragma unroll
+          for (int it = 0; it < 2; ++it)
+            if (ok[4 * it])
+              *(float4_t*)(orow + 4 * lane + 256 * it) =
+                  float4_t{v[c][4 * it], v[c][4 * it + 1], v[c][4 * it + 2], v[c][4 * it + 3]};
+        } else {
+#pragma unroll
+          for (int p = 0; p < 8; ++p)
+            if (ok[p]) orow[lane + 64 * p] = v[c][p];
+        }
       }
     }
   }
@@ -334,8 +422,12 @@ extern "C" int aaclip_patch_scores(int in_dtype, const void* const* levels, int 
     lv.p[i] = levels[i];
   }
   if (rows == 0) return AACLIP_OK;
-  patch_scores_kernel<<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
-      in_dtype, lv, n_levels, ld, T, rows, normalize, mode, mode == 1 ? group : 1, out);
+  if (in_dtype == AACLIP_F32)
+    patch_scores_kernel<true><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
+        lv, n_levels, ld, T, rows, normalize, mode, mode == 1 ? group : 1, out);
+  else
+    patch_scores_kernel<false><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
+        lv, n_levels, ld, T, rows, normalize, mode, mode == 1 ? group : 1, out);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -352,6 +444,26 @@ extern "C" int aaclip_patch_logits(int in_dtype, const void* f, int64_t ld, cons
   return AACLIP_OK;
 }
 
+// Launch stage 2 for (C, ksize): rows of LDS the band needs, sized on the host.
+template <int C>
+int launch_blur_upsample(const float* grid, float* out, int batch, int g, int S, int ksize, const Gauss& gw,
+                         int softmax, float scale, hipStream_t s) {
+  const int span = (int)(scale * (float)(kBand - 1)) + 4;  // source rows a band's taps can reach (+1 margin)
+  const int brows = min(g, span);
+  const int xrows = min(g, brows + 2 * (ksize / 2));
+  const size_t lds = (size_t)C * (2 * xrows + brows) * g * sizeof(float);
+  if (lds > 64 * 1024) return AACLIP_ERR_ARG;
+  const dim3 grd(ceil_div(S, kBand), batch);
+#define BU_LAUNCH(K) \
+  blur_upsample_kernel<C, K><<<grd, 64, lds, s>>>(grid, out, g, S, ksize, gw, softmax, scale, xrows, brows)
+  if (ksize == 0) BU_LAUNCH(0);
+  else if (ksize == 7) BU_LAUNCH(7);
+  else if (ksize == 9) BU_LAUNCH(9);
+  else BU_LAUNCH(-1);
+#undef BU_LAUNCH
+  return AACLIP_OK;
+}
+
 extern "C" int aaclip_blur_upsample(const float* grid, float* out, int batch, int channels, int g,
                                     int out_size, int ksize, float sigma, int softmax,
                                     void* stream) {
@@ -360,14 +472,19 @@ extern "C" int aaclip_blur_upsample(const float* grid, float* out, int batch, in
   AACLIP_REQUIRE(ksize >= 0 && ksize <= 15 && (ksize == 0 || (ksize % 2 == 1 && ksize / 2 < g)));
   const Gauss gw = ksize > 0 ? gaussian_weights(ksize, sigma) : Gauss{};
   const float scale = (float)(g - 1) / (float)(out_size - 1);
-  const size_t lds = (size_t)(ksize > 0 ? 2 : 1) * channels * g * g * sizeof(float);
-  AACLIP_REQUIRE(lds <= 160 * 1024);
-  static unsigned attr_dev = 0;
-  if (lds > 64 * 1024 && !lds_attr_once((const void*)blur_upsample_kernel, 160 * 1024, attr_dev))
-    return AACLIP_ERR_LAUNCH;
-  dim3 grd(ceil_div(out_size, kBand), batch);
-  blur_upsample_kernel<<<grd, 256, lds, (hipStream_t)stream>>>(grid, out, channels, g, out_size,
-                                                               ksize, gw, softmax, scale);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = AACLIP_ERR_ARG;
+  switch (channels) {
+    case 1: rc = launch_blur_upsample<1>(grid, out, batch, g, out_size, ksize, gw, softmax, scale, s); break;
+    case 2: rc = launch_blur_upsample<2>(grid, out, batch, g, out_size, ksize, gw, softmax, scale, s); break;
+    case 3: rc = launch_blur_upsample<3>(grid, out, batch, g, out_size, ksize, gw, softmax, scale, s); break;
+    case 4: rc = launch_blur_upsample<4>(grid, out, batch, g, out_size, ksize, gw, softmax, scale, s); break;
+    case 5: rc = launch_blur_upsample<5>(grid, out, batch, g, out_size, ksize, gw, softmax, scale, s); break;
+    case 6: rc = launch_blur_upsample<6>(grid, out, batch, g, out_size, ksize, gw, softmax, scale, s); break;
+    case 7: rc = launch_blur_upsample<7>(grid, out, batch, g, out_size, ksize, gw, softmax, scale, s); break;
+    default: rc = launch_blur_upsample<8>(grid, out, batch, g, out_size, ksize, gw, softmax, scale, s); break;
+  }
+  if (rc) return rc;
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

@@ -215,8 +215,8 @@ def roofline_map(eng, ws, T, reps=50):
     S = ws["map"].shape[-1]
     g = ws["g"]
     t_all = time_launches(lambda: ops.anomaly_map(seg, T, ws["map"], ws["grid"], g=g, ksize=7, sigma=1.0), reps, s)
-    t_ps = time_launches(lambda: ops.patch_scores(seg, T, ws["grid"]), reps, s)
-    t_bu = time_launches(lambda: ops.blur_upsample(ws["grid"].view(B, 1, g, g), ws["map"].view(B, 1, S, S),
+    t_ps = time_launches(lambda: ops.patch_scores(seg, T, ws["grid"][:rows]), reps, s)
+    t_bu = time_launches(lambda: ops.blur_upsample(ws["grid"][:rows].view(B, 1, g, g), ws["map"].view(B, 1, S, S),
                                                    ksize=7, sigma=1.0), reps, s)
     read1 = len(seg) * rows * 768 * seg[0].element_size() + 768 * 2 * 4
     write2 = B * S * S * 4

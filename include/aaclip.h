@@ -274,7 +274,7 @@ int aaclip_blur_upsample(const float* grid, float* out, int batch, int channels,
 
 /*
  * Full test-branch anomaly map for one batch: patch_scores (mode 0) into the
- * caller's workspace grid_ws [batch*g*g] fp32, then blur + upsample into
+ * caller's workspace grid_ws (>= batch*g*g fp32), then blur + upsample into
  * out [batch, S, S]. Replaces: test.py:86-93 + forward_utils.py:196-213.
  */
 int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n_levels, int64_t ld,

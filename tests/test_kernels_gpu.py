@@ -431,3 +431,24 @@ def test_blur_upsample_train_softmax_any_size(dev, S):
     ops.blur_upsample(torch.from_numpy(grid).to(dev), out, ksize=0, sigma=0.0, softmax=True)
     ref = R.softmax(R.upsample_bilinear_ac(grid, S), axis=1)
     np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,g,S,L,dom", [(3, 24, 336, 4, "Industrial"), (2, 37, 518, 4, "Medical"),
+                                         (2, 32, 448, 6, "Medical"), (5, 8, 41, 1, "Industrial")])
+def test_anomaly_map_equals_stages(dev, dt, B, g, S, L, dom):
+    """aaclip_anomaly_map is bit-identical to patch_scores + blur_upsample, launch after
+    launch, at the C2 / 518 / C5 shapes and a ragged small one."""
+    torch.manual_seed(B * g + S)
+    lv = [torch.randn(B * g * g, 768, device=dev).to(dt) for _ in range(L)]
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev), dim=0).contiguous()
+    k, s = (7, 1.0) if dom == "Industrial" else (9, 1.5)
+    grid2 = torch.empty(B * g * g, device=dev)
+    ops.patch_scores(lv, T, grid2)
+    ref = torch.empty(B, 1, S, S, device=dev)
+    ops.blur_upsample(grid2.view(B, 1, g, g), ref, ksize=k, sigma=s)
+    ws = torch.empty(B * g * g, device=dev)
+    for _ in range(3):
+        out = torch.full((B, S, S), float("nan"), device=dev)
+        ops.anomaly_map(lv, T, out, ws, g=g, ksize=k, sigma=s)
+        assert torch.equal(out, ref[:, 0])
