@@ -39,6 +39,7 @@ SIGNATURES = {
     "aaclip_gemm_fp8mx": [_I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _P, _P, _L, _P, _L, _P, _L, _P],
     "aaclip_quant_fp8_mx": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _P],
     "aaclip_set_gemm_variant": [_I],
+    "aaclip_gemm_pin": [_I, _I, _I, _I, _I],
     "aaclip_gemm_plan": [_I, _I, _I, _I],
     "aaclip_attention": [_I, _P, _P, _I, _I, _I, _I, _I, _P, _L, _P],
     "aaclip_im2col": [_I, _P, _P, _I, _I, _I, _I, _I, _P],

@@ -21,6 +21,8 @@ conv1 flattened to [1024, 640] (K padded 588 -> 640 with zeros).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
@@ -35,6 +37,9 @@ PATCH = 14
 EMBED = 768
 KPATCH = 640  # 3*14*14 = 588 padded to a multiple of 64
 DOMAIN_BLUR = {"Industrial": (7, 1.0), "Medical": (9, 1.5)}
+# measure + pin the GEMM tile family per block-GEMM shape at workspace creation
+# (ops.tune_gemm); AACLIP_GEMM_TUNE=0 keeps the built-in heuristic
+TUNE = os.environ.get("AACLIP_GEMM_TUNE", "1") != "0"
 
 
 def _on_device(fn):
@@ -203,7 +208,27 @@ class VisualEngine:
         for k in chunk_keys[:max(0, len(chunk_keys) - (WS_KEEP - 1))]:
             del self._ws[k]
         self._ws[key] = ws
+        if TUNE and cdt != torch.float32:
+            self._tune(ws)
         return ws
+
+    def _tune(self, ws):
+        """Pin the fastest tile family for each 16-bit block-GEMM shape of this
+        workspace (ops.tune_gemm: measured once per shape and process, on the
+        workspace's own buffers and epilogues; bit-neutral). Runs when a workspace
+        is first created, i.e. outside any graph capture (graphed_predict warms up
+        eagerly first)."""
+        blk, X, H = self.blocks[0], ws["x"], ws["h"]
+        scratch = torch.empty_like(X)
+        if not (self.fp8 and not self.fp8_mlp_only):
+            ops.tune_gemm(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
+            ops.tune_gemm(ws["attn"], blk["w_o"], scratch, bias=blk["b_o"], residual=scratch)
+        if not self.fp8:
+            ops.tune_gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True)
+            ops.tune_gemm(ws["fc"], blk["w_pr"], scratch, bias=blk["b_pr"], residual=scratch, aux=ws["xb"])
+        if self.adapt_until > 0:
+            ops.tune_gemm(ws["xb"], self.w_adapt[0], ws["u"], leaky=True)
+        del scratch
 
     # ------------------------------------------------------------------ forward
     @torch.no_grad()

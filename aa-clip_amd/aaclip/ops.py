@@ -85,6 +85,48 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
     return out
 
 
+# tile families aaclip_gemm_pin accepts (include/aaclip.h): 8-phase 256x256, 320x256,
+# 256x256, 128x128, 256x128
+GEMM_FAMILIES = (3, 8, 1, 9, 2)
+_tuned = {}
+
+
+def tune_gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, reps: int = 3, **epilogue) -> int:
+    """Measure every tile family on these operands with this epilogue (HIP events on the
+    current stream) and pin the fastest for the shape (aaclip_gemm_pin). The families
+    accumulate K in the same order, so the pin changes speed, never bits. Host-side
+    setup only (it synchronises): never call it while a hipGraph is being captured.
+    Returns the pinned family; shapes already tuned in this process are skipped."""
+    if a.dtype not in (torch.bfloat16, torch.float16):
+        return 0
+    M, K = a.shape
+    N = w.shape[0]
+    key = (dtag(a), M, N, K)
+    if key in _tuned:
+        return _tuned[key]
+    st = torch.cuda.current_stream()
+    best, best_t = 0, float("inf")
+    try:
+        for fam in GEMM_FAMILIES:
+            if fam != 2 and N % 256:
+                continue
+            call("aaclip_gemm_pin", key[0], M, N, K, fam)
+            gemm(a, w, out, **epilogue)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(reps):
+                gemm(a, w, out, **epilogue)
+            e1.record(st)
+            e1.synchronize()
+            t = e0.elapsed_time(e1)
+            if t < best_t:
+                best, best_t = fam, t
+    finally:
+        call("aaclip_gemm_pin", key[0], M, N, K, best)
+    _tuned[key] = best
+    return best
+
+
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), one byte per element
 
 

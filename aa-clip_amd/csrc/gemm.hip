@@ -929,18 +929,34 @@ int g_group_m = 8;
 int g_setprio = 0;
 int g_dbg = 0;
 
+// Per-shape pinned tile family (aaclip_gemm_pin): measured choice for a (dtype, M, N, K)
+// that overrides the heuristic. Written at engine setup (host), read by every launch.
+struct Pin {
+  int dtype, M, N, K, fam;
+};
+constexpr int kPins = 256;
+Pin g_pins[kPins];
+int g_npins = 0;
+
+int pinned_family(int dtype, int M, int N, int K) {
+  for (int i = 0; i < g_npins; ++i)
+    if (g_pins[i].dtype == dtype && g_pins[i].M == M && g_pins[i].N == N && g_pins[i].K == K) return g_pins[i].fam;
+  return 0;
+}
+
 // 16-bit dispatch (bf16 or fp16 operands; same tiles, same per-shape choice)
 template <bool H16>
 int dispatch16(GemmArgs a, hipStream_t s) {
   const int M = a.M, N = a.N;
   if (a.K % 64 || N % 128) return AACLIP_ERR_ARG;
   const bool fits = (int64_t)M * a.lda * 2 < (1ll << 31) && (int64_t)N * a.ldw * 2 < (1ll << 31);
-  switch (g_gemm_variant) {
+  const int fam = g_gemm_variant ? g_gemm_variant : pinned_family(H16 ? AACLIP_F16 : AACLIP_BF16, M, N, a.K);
+  switch (fam) {
     case 1: return launch_bf16<256, 256, 2, 4, 0, H16>(a, s);
     case 2: return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
     case 3:
     case 4:  // 8-phase for the wide GEMMs only (N >= 2048), 320x256 below
-      if (N % 256 == 0 && (g_gemm_variant == 3 || N >= 2048) && fits) return launch_bf16_8ph<H16>(a, s);
+      if (N % 256 == 0 && (fam == 3 || N >= 2048) && fits) return launch_bf16_8ph<H16>(a, s);
       break;
     case 9: return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);  // 128x128 everywhere (A/B)
     case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
@@ -954,7 +970,7 @@ int dispatch16(GemmArgs a, hipStream_t s) {
   // pipeline (16 images per stream, M = 9232) the 8-phase kernel wins on QKV, out-proj,
   // c_proj and adapters (148-444 tiles) and the 320-row one on c_fc (464 vs 592 tiles
   // = 2 vs 3 rounds); measured per shape with tools/kbench.py, whole C2 step +5 %.
-  if (N % 256 == 0 && g_gemm_variant == 0) {
+  if (N % 256 == 0 && fam == 0) {
     const bool ph8 = fits && prefer_8ph(M, N);
     if (prefer_small(M, N, ph8)) return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);
     if (ph8) return launch_bf16_8ph<H16>(a, s);
@@ -970,25 +986,41 @@ int dispatch16(GemmArgs a, hipStream_t s) {
 extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
   if (in_dtype != AACLIP_BF16 && in_dtype != AACLIP_F16) return "gemm_f32_kernel";
   if (M <= 0 || N % 128 || K % 64) return "invalid";
-  switch (g_gemm_variant) {
+  const int fam = g_gemm_variant ? g_gemm_variant : pinned_family(in_dtype, M, N, K);
+  switch (fam) {
     case 1: return "gemm_bf16_kernel<256,256,2,4>";
     case 2: return "gemm_bf16_kernel<256,128,4,2>";
     case 3:
     case 4:
-      if (N % 256 == 0 && (g_gemm_variant == 3 || N >= 2048)) return "gemm_bf16_8ph_kernel<256,256>";
+      if (N % 256 == 0 && (fam == 3 || N >= 2048)) return "gemm_bf16_8ph_kernel<256,256>";
       break;
     case 8:
       if (N % 256 == 0) return "gemm_bf16_kernel<320,256,2,4>";
       break;
     default: break;
   }
-  if (N % 256 == 0 && g_gemm_variant == 0) {
+  if (N % 256 == 0 && fam == 0) {
     const bool ph8 = prefer_8ph(M, N);
     if (prefer_small(M, N, ph8)) return "gemm_bf16_kernel<128,128,2,2>";
     if (ph8) return "gemm_bf16_8ph_kernel<256,256>";
   }
-  if (g_gemm_variant == 9) return "gemm_bf16_kernel<128,128,2,2>";
+  if (fam == 9) return "gemm_bf16_kernel<128,128,2,2>";
   return N % 256 == 0 ? "gemm_bf16_kernel<320,256,2,4>" : "gemm_bf16_kernel<256,128,4,2>";
+}
+
+extern "C" int aaclip_gemm_pin(int in_dtype, int M, int N, int K, int family) {
+  AACLIP_REQUIRE((in_dtype == AACLIP_BF16 || in_dtype == AACLIP_F16) && M > 0 && N > 0 && K > 0);
+  AACLIP_REQUIRE(family == 0 || family == 1 || family == 2 || family == 3 || family == 8 || family == 9);
+  AACLIP_REQUIRE(family == 0 || family == 2 || N % 256 == 0);
+  for (int i = 0; i < g_npins; ++i)
+    if (g_pins[i].dtype == in_dtype && g_pins[i].M == M && g_pins[i].N == N && g_pins[i].K == K) {
+      g_pins[i].fam = family;
+      return AACLIP_OK;
+    }
+  if (family == 0) return AACLIP_OK;
+  AACLIP_REQUIRE(g_npins < kPins);
+  g_pins[g_npins++] = Pin{in_dtype, M, N, K, family};
+  return AACLIP_OK;
 }
 
 extern "C" int aaclip_set_gemm_variant(int variant) {

@@ -4,7 +4,9 @@ Test transform (reference :127-143): PIL bicubic resize to (S, S) -> [0,1]
 tensor -> CLIP mean/std normalise; masks: nearest resize -> (mask != 0).
 Implemented with PIL + numpy (torchvision is not in this image). Metadata is the
 reference's jsonl layout, `./dataset/metadata/<dataset>/full-shot.jsonl`
-relative to the working directory, images under DATA_PATH[dataset].
+relative to the working directory (or under $AACLIP_METADATA_ROOT, e.g. the
+reference checkout's dataset/metadata — the lists are not shipped here), images
+under DATA_PATH[dataset].
 
 Extra: dataset name "synthetic" (no files needed) yields seeded N(0,1)
 post-normalisation images and rectangle masks.
@@ -118,6 +120,18 @@ def collate_raw(items):
     return out
 
 
+def metadata_root() -> str:
+    """Where the per-dataset jsonl test lists live. The reference reads
+    ./dataset/metadata relative to the working directory (dataset/__init__.py:204);
+    the same relative path is used here when it exists, else $AACLIP_METADATA_ROOT
+    (e.g. <reference checkout>/dataset/metadata: the lists ship with the reference,
+    not with this build)."""
+    local = "./dataset/metadata"
+    if os.path.isdir(local) or "AACLIP_METADATA_ROOT" not in os.environ:
+        return local
+    return os.environ["AACLIP_METADATA_ROOT"]
+
+
 def get_dataset(dataset_name: str, img_size: int, training_mode: str, shot: int = -1, stage: str = "train",
                 logger=None, synthetic_n: int = 16, raw: bool = False):
     if dataset_name in ("synthetic", "synthetic_mvtec"):
@@ -134,7 +148,7 @@ def get_dataset(dataset_name: str, img_size: int, training_mode: str, shot: int 
     if stage == "train":
         raise NotImplementedError("training datasets are out of scope (inference path only)")
     if stage in ("test", "visualize"):
-        meta_path = os.path.join("./dataset/metadata", dataset_name, "full-shot.jsonl")
+        meta_path = os.path.join(metadata_root(), dataset_name, "full-shot.jsonl")
         return {c: BaseSingleClassDataset(DATA_PATH[dataset_name], meta_path, img_size, c,
                                           logger=logger if stage == "test" else None, raw=raw)
                 for c in CLASS_NAMES[dataset_name]}

@@ -183,6 +183,17 @@ def _fp16_round_openai(model: nn.Module, state_dict: dict) -> dict:
     return out
 
 
+def _is_torchscript(path: str) -> bool:
+    import zipfile
+    try:
+        with zipfile.ZipFile(path) as z:
+            names = z.namelist()
+    except (zipfile.BadZipFile, OSError):
+        return False
+    return any(n.endswith("constants.pkl") for n in names) and any("/code/" in n or n.startswith("code/")
+                                                                   for n in names)
+
+
 def load_openai_state_dict(path: str) -> dict:
     """OpenAI ViT-L-14-336px.pt: a TorchScript archive (reference model/openai.py:56-65);
     read its tensors with torch.jit.load, or a plain state dict with weights_only."""
@@ -193,6 +204,10 @@ def load_openai_state_dict(path: str) -> dict:
         if isinstance(sd, dict) and "state_dict" in sd:
             sd = sd["state_dict"]
     except Exception:
+        # only a TorchScript archive (the OpenAI release format: code/ + constants.pkl)
+        # goes to torch.jit.load; a corrupt / truncated / other file keeps its error
+        if not _is_torchscript(path):
+            raise
         sd = torch.jit.load(path, map_location="cpu").state_dict()
     for k in ("input_resolution", "context_length", "vocab_size"):
         sd.pop(k, None)

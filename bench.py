@@ -112,14 +112,28 @@ def flops_per_image(n_tok=577, levels=4, adapt=6):
     return blocks + 2 * P * 588 * W + adapt * 2 * n_tok * W * W + levels * 2 * P * W * 768 + 2 * P * W * 768
 
 
-def time_launches(fn, reps, stream):
+def time_launches(fn, reps, stream=None):
+    """GPU time per launch of fn (ms): `reps` launches captured into one hipGraph and
+    replayed between HIP events on the replay stream, so host launch overhead (ctypes,
+    argument checks) is not in the number; the dependent-kernel boundary (~1.5 us) is."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        fn()  # warm-up outside the capture (kernel attributes, lazy allocations)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(reps):
+            fn()
+    graph.replay()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
-    fn()
-    start.record(stream)
-    for _ in range(reps):
-        fn()
-    end.record(stream)
+    start.record(st)
+    graph.replay()
+    end.record(st)
     end.synchronize()
     return start.elapsed_time(end) / reps  # ms per launch
 
@@ -129,7 +143,15 @@ def latency_b1(eng, size, T, reps=30):
     hipGraph replay, input already on device; HIP events on the replay stream."""
     run = eng.graphed_predict(1, size, "Industrial", streams=1)
     x = torch.randn(1, 3, size, size, device=T.device)
-    ms = time_launches(lambda: run(x, T), reps, torch.cuda.current_stream())
+    st = torch.cuda.current_stream()
+    run(x, T)
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record(st)
+    for _ in range(reps):
+        run(x, T)
+    end.record(st)
+    end.synchronize()
+    ms = start.elapsed_time(end) / reps
     return {"batch": 1, "ms_per_image": round(ms, 3), "images_per_sec": round(1e3 / ms, 1)}
 
 

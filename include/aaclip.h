@@ -137,6 +137,15 @@ int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int
  */
 int aaclip_set_gemm_variant(int variant);
 
+/*
+ * Pin the tile family aaclip_gemm uses for one (in_dtype, M, N, K) (bf16 / f16):
+ * 1 = 256x256, 2 = 256x128, 3 = 256x256 8-phase ping-pong, 8 = 320x256,
+ * 9 = 128x128, 0 = unpin (back to the heuristic). Set by a measuring tuner at
+ * engine setup (aaclip/ops.py tune_gemm); every family accumulates K in the same
+ * order, so a pin changes speed, never bits. Process-global, host only.
+ */
+int aaclip_gemm_pin(int in_dtype, int M, int N, int K, int family);
+
 /* Name of the kernel aaclip_gemm launches for (in_dtype, M, N, K) under the current
  * variant (the default dispatch's per-shape choice). Host only, for reports. */
 const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K);

@@ -97,3 +97,16 @@ def test_metrics_eval_matches_reference(golden):
         r = metrics_eval(o["met_masks"], o["met_labels"], o["met_pp"].copy(), o["met_ip"].copy(), "synthetic", dom)
         for k in ("pixel AUC", "pixel AP", "image AUC", "image AP"):
             assert r[k] == pytest.approx(ref[dom][k], abs=1e-9)
+
+
+def test_metadata_root_env(monkeypatch, tmp_path):
+    """Without ./dataset/metadata in the working directory the jsonl lists are looked up
+    under $AACLIP_METADATA_ROOT (the reference checkout's dataset/metadata)."""
+    import dataset
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.delenv("AACLIP_METADATA_ROOT", raising=False)
+    assert dataset.metadata_root() == "./dataset/metadata"
+    monkeypatch.setenv("AACLIP_METADATA_ROOT", "/some/reference/dataset/metadata")
+    assert dataset.metadata_root() == "/some/reference/dataset/metadata"
+    (tmp_path / "dataset" / "metadata").mkdir(parents=True)
+    assert dataset.metadata_root() == "./dataset/metadata"

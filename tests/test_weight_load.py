@@ -41,3 +41,15 @@ def test_missing_checkpoint_raises(monkeypatch, tmp_path):
     monkeypatch.setitem(clip._MODEL_CKPT_PATHS, "ViT-L-14-336", str(tmp_path / "absent.pt"))
     with pytest.raises(RuntimeError, match="not found"):
         clip.create_model("ViT-L-14-336", 336, pretrained="openai")
+
+
+def test_corrupt_checkpoint_keeps_its_error(monkeypatch, tmp_path):
+    """A file that is neither a weights-only state dict nor a TorchScript archive is
+    not handed to torch.jit.load: the weights-only loader's own error surfaces."""
+    import model.clip as clip
+    bad = tmp_path / "ViT-L-14-336px.pt"
+    bad.write_bytes(b"\x00not a checkpoint" * 64)
+    monkeypatch.setitem(clip._MODEL_CKPT_PATHS, "ViT-L-14-336", str(bad))
+    with pytest.raises(Exception) as e:
+        clip.create_model("ViT-L-14-336", 336, pretrained="openai")
+    assert "jit" not in type(e.value).__module__ and "TorchScript" not in str(e.value)
