@@ -42,6 +42,7 @@ SIGNATURES = {
     "aaclip_gemm_pin": [_I, _I, _I, _I, _I],
     "aaclip_gemm_plan": [_I, _I, _I, _I],
     "aaclip_attention": [_I, _P, _P, _I, _I, _I, _I, _I, _P, _L, _P],
+    "aaclip_set_attn_variant": [_I],
     "aaclip_im2col": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "aaclip_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],
     "aaclip_block_tail": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],

@@ -38,8 +38,9 @@ EMBED = 768
 KPATCH = 640  # 3*14*14 = 588 padded to a multiple of 64
 DOMAIN_BLUR = {"Industrial": (7, 1.0), "Medical": (9, 1.5)}
 # measure + pin the GEMM tile family per block-GEMM shape at workspace creation
-# (ops.tune_gemm); AACLIP_GEMM_TUNE=0 keeps the built-in heuristic
-TUNE = os.environ.get("AACLIP_GEMM_TUNE", "1") != "0"
+# (ops.tune_gemm) when AACLIP_GEMM_TUNE=1. Off by default: in the two-stream C2 pipeline the
+# isolated ranking does not carry over (tools/pin_search.py: the heuristic ~= the best pins)
+TUNE = os.environ.get("AACLIP_GEMM_TUNE", "0") == "1"
 
 
 def _on_device(fn):

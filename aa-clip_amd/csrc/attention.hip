@@ -23,9 +23,6 @@ namespace {
 
 constexpr int HD_ = 64;      // head dim
 constexpr int KT = 64;       // keys per tile
-constexpr int QW = 32;       // queries per wave
-constexpr int NW = 4;        // waves per workgroup
-constexpr int QT = QW * NW;  // queries per workgroup
 
 __device__ __forceinline__ short4_t tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(p));
@@ -64,9 +61,9 @@ __device__ __forceinline__ float max_over_groups(float v) {
 constexpr float kRescaleLog2 = 8.0f;
 
 template <int NKB, int NQB, bool MASK, bool H16>
-__device__ __forceinline__ void attn_tile(const char* kt_lds, const h16x8_t<H16> (&qf)[2][2], float4_t (&ot)[2][4],
-                                          float (&m_run)[2], float4_t (&l_acc)[2], int key0, int q0, int N,
-                                          int causal, int g, int c, bool first) {
+__device__ __forceinline__ void attn_tile(const char* kt_lds, const h16x8_t<H16> (&qf)[NQB][2],
+                                          float4_t (&ot)[NQB][4], float (&m_run)[NQB], float4_t (&l_acc)[NQB],
+                                          int key0, int q0, int N, int causal, int g, int c, bool first) {
   using V8 = h16x8_t<H16>;
   using E = h16_t<H16>;
   const char* vt_lds = kt_lds + KT * 128;
@@ -172,14 +169,32 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const h16x8_t<H16>
 #define ATTN_OCC 3  // workgroups per CU the register budget is sized for
 #endif
 
+// Counted wait for the K/V ring + workgroup barrier: PIECES = LDS-DMA pieces one
+// wave issues per stage (K and V), i.e. how many may stay in flight (the newest stage).
+template <int PIECES>
+__device__ __forceinline__ void wait_barrier(bool deep) {
+  if (!deep)
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (PIECES == 4)
+    asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+  else if constexpr (PIECES == 8)
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else
+    static_assert(PIECES == 4 || PIECES == 8, "pieces per wave per stage");
+}
+
 // H16: fp16 q/k/v/p on v_mfma_f32_16x16x32_f16 (the parity-grade mode), else bf16.
-template <bool H16>
-__global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t* __restrict__ qkv,
-                                                        uint16_t* __restrict__ out, int batch, int N, int H,
-                                                        int flags, uint8_t* __restrict__ out_mx,
-                                                        int64_t ld_mx) {
+// QB 16-query blocks per wave, NW waves per workgroup (QT = 16 * QB * NW queries),
+// NS-stage K/V ring. Every wave reads the whole K and V tile from LDS, so queries
+// per wave set the LDS bytes per FLOP: QB = 4 halves them against QB = 2.
+template <bool H16, int QB, int NW, int NS>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_kernel(
+    const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int batch, int N, int H, int flags,
+    uint8_t* __restrict__ out_mx, int64_t ld_mx) {
   const int causal = flags & AACLIP_ATTN_CAUSAL;
-  constexpr int NS = ATTN_STAGES;
+  constexpr int QW = 16 * QB;     // queries per wave
+  constexpr int QT = QW * NW;     // queries per workgroup
+  constexpr int PR = 64 / (8 * NW);  // 8-row DMA pieces per wave per K (and per V) tile
   // the prologue fills NS-1 <= 2 stages and the counted waits assume <= 2 tiles in
   // flight: a 4-stage ring would read a never-filled slot (measured: checksums
   // differ run to run), so only 2 and 3 are valid
@@ -207,9 +222,9 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   const int q0 = qtile * QT + wid * QW;
 
   // ---- Q fragments (B operand of K.Q^T): lane holds Q[q][ks*32 + 8g .. +7]
-  V8 qf[2][2];
+  V8 qf[QB][2];
 #pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+  for (int qb = 0; qb < QB; ++qb) {
     const int q = min(q0 + qb * 16 + c, N - 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) qf[qb][ks] = *(const V8*)(base + (size_t)q * ld + ks * 32 + 8 * g);
@@ -217,7 +232,7 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   if (!(flags & AACLIP_ATTN_Q_PRESCALED)) {  // log2(e)/sqrt(64) not folded by the caller: apply it here
     constexpr float sl2 = 0.125f * 1.4426950408889634f;
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
+    for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -232,9 +247,11 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   const int64_t head0 = (int64_t)b * N * ld + h * HD_;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(qkv + head0), 0, (int)(((int64_t)batch * N * ld - head0) * 2), 0x00020000);
-  int voff[2];
+  int voff[4];  // PR <= 4 used (fixed size: a template-dependent array captured by the staging
+               // lambda makes clang's host pass drop the kernel's instantiation)
+  static_assert(PR <= 4, "DMA pieces per wave");
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < PR; ++i) {
     const int r = (i * NW + wid) * 8 + (lane >> 3);
     const int chunk = (lane & 7) ^ (r & 7);
     voff[i] = (int)(r * ld + HDt + chunk * 8) * 2;
@@ -245,20 +262,23 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     char* vb = kb + KT * 128;
     const int so = t * KT * row_bytes;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 64 / (8 * NW); ++i) {  // PR pieces (template expression: no capture in the lambda)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(kb + (i * NW + wid) * 1024), 16, voff[i], so, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(vb + (i * NW + wid) * 1024), 16, voff[i], so + v_off,
                                                0, 0);
     }
   };
 
-  float4_t ot[2][4];
+  float4_t ot[QB][4];
+  float m_run[QB];     // set from the first tile (attn_tile first = true)
+  float4_t l_acc[QB];  // row sums (MFMA)
 #pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
+  for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
     for (int db = 0; db < 4; ++db) ot[qb][db] = float4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {0.f, 0.f};  // set from the first tile (attn_tile first = true)
-  float4_t l_acc[2] = {float4_t{0.f, 0.f, 0.f, 0.f}, float4_t{0.f, 0.f, 0.f, 0.f}};  // row sums (MFMA)
+    m_run[qb] = 0.f;
+    l_acc[qb] = float4_t{0.f, 0.f, 0.f, 0.f};
+  }
 
   int ntiles = (N + KT - 1) / KT;
   if (causal) {
@@ -276,10 +296,9 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   // Ring of NS K/V stages: tile t+NS-1 is issued while tile t is computed; the
   // end-of-tile wait is COUNTED (vmcnt retires in order, 4 DMAs per wave per
   // stage) so tiles t+2.. stay in flight across the barrier.
-#define ATTN_WAIT_BARRIER(n) asm volatile("s_waitcnt vmcnt(" #n ")\n\ts_barrier" ::: "memory")
   stage(0, 0);
   if (NS > 2 && ntiles > 1) stage(1, 1);
-  if (NS > 2 && ntiles > 1) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
+  wait_barrier<2 * PR>(NS > 2 && ntiles > 1);
   // Waves always compute both 16-query blocks (rows past N are clamped copies,
   // discarded at the store); a wave with no valid query skips the math but keeps
   // staging and barriers. Full tiles (no key tail, no causal cut for any wave of
@@ -299,9 +318,9 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
   for (; t < nfull; ++t) {
     const bool deep = advance();
     if (active)
-      attn_tile<4, 2, false, H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g, c,
-                             t == 0);
-    if (deep) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
+      attn_tile<4, QB, false, H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g, c,
+                                   t == 0);
+    wait_barrier<2 * PR>(deep);
     cur = cur + 1 == NS ? 0 : cur + 1;
   }
   for (; t < ntiles; ++t) {
@@ -311,14 +330,13 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     const int live = min(KT, N - key0);  // valid keys in this tile
     if (active) {
       const bool first = t == 0;
-      if (live > 32) attn_tile<4, 2, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
-      else if (live > 16) attn_tile<2, 2, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
-      else attn_tile<1, 2, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
+      if (live > 32) attn_tile<4, QB, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
+      else if (live > 16) attn_tile<2, QB, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
+      else attn_tile<1, QB, true, H16>(kt_lds, qf, ot, m_run, l_acc, key0, q0, N, causal, g, c, first);
     }
-    if (deep) ATTN_WAIT_BARRIER(4); else ATTN_WAIT_BARRIER(0);
+    wait_barrier<2 * PR>(deep);
     cur = cur + 1 == NS ? 0 : cur + 1;
   }
-#undef ATTN_WAIT_BARRIER
   if (ntiles == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prologue's tile-0 DMA
 
   if (tail_inline && active) {
@@ -338,7 +356,7 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
         vv[db][3] = h16_to_f32<H16>((uint16_t)(w.y >> 16));
       }
 #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
+      for (int qb = 0; qb < QB; ++qb) {
         float sp = 0.f;  // this lane's 16 of the 64 dims (Q prescaled: log2 domain)
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -366,7 +384,7 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     // RNE e4m3, 4x4 dword transpose so lane g owns columns 16g..16g+15 -> 16-B stores
     uint8_t* o8 = (uint8_t*)out;
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 0; qb < QB; ++qb) {
       const float inv = 1.0f / l_acc[qb][0];
       const int q = q0 + qb * 16 + c;
       float amax = 0.f;
@@ -411,7 +429,7 @@ __global__ __launch_bounds__(256, ATTN_OCC) void attn_bf16_kernel(const uint16_t
     return;
   }
 #pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+  for (int qb = 0; qb < QB; ++qb) {
     const float inv = 1.0f / l_acc[qb][0];
     const int q = q0 + qb * 16 + c;
     if (q < N) {
@@ -494,7 +512,25 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(const float* __restrict__ 
   }
 }
 
+// 1 = 4 waves x 32 queries (3-stage ring, 3 workgroups per CU), 2 = 2 waves x 64
+// queries (2-stage ring, 4 workgroups per CU: half the LDS bytes per FLOP)
+constexpr int kAttnDefault = 1;
+int g_attn_variant = 0;
+
+template <bool H16, int QB, int NW, int NS>
+void launch_attn(const uint16_t* q, uint16_t* o, int batch, int seq, int heads, int flags, uint8_t* mx, int64_t ld_mx,
+                 hipStream_t s) {
+  const long nwg = (long)ceil_div(seq, 16 * QB * NW) * batch * heads;
+  attn_bf16_kernel<H16, QB, NW, NS><<<(unsigned)nwg, 64 * NW, 0, s>>>(q, o, batch, seq, heads, flags, mx, ld_mx);
+}
+
 }  // namespace
+
+extern "C" int aaclip_set_attn_variant(int variant) {
+  AACLIP_REQUIRE(variant >= 0 && variant <= 2);
+  g_attn_variant = variant;
+  return AACLIP_OK;
+}
 
 extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
                                 int heads, int head_dim, int flags, void* out_mx, int64_t ld_mx,
@@ -506,16 +542,20 @@ extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch
   AACLIP_REQUIRE((int64_t)batch * seq * 3 * heads * HD_ * 2 < (1ll << 31));  // buffer-descriptor range
   AACLIP_REQUIRE(dtype != AACLIP_FP8 || (out_mx && ld_mx >= (int64_t)batch * seq && heads % 2 == 0));
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == AACLIP_F16) {  // fp16 compute (parity-grade 16-bit mode)
-    const long nwg = (long)ceil_div(seq, QT) * batch * heads;
+  if (dtype != AACLIP_F32) {  // bf16 / fp16 compute; fp8 = bf16 inputs with an MX e4m3 output
+    const int v = g_attn_variant ? g_attn_variant : kAttnDefault;
+    const long nwg = (long)ceil_div(seq, 128) * batch * heads;  // every variant: 128 queries per workgroup
     AACLIP_REQUIRE(nwg < (1L << 31));
-    attn_bf16_kernel<true><<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, batch, seq, heads,
-                                                         flags, nullptr, 0);
-  } else if (dtype != AACLIP_F32) {  // bf16 compute; fp8 = bf16 inputs with an MX e4m3 output
-    const long nwg = (long)ceil_div(seq, QT) * batch * heads;
-    AACLIP_REQUIRE(nwg < (1L << 31));
-    attn_bf16_kernel<false><<<(unsigned)nwg, 256, 0, s>>>((const uint16_t*)qkv, (uint16_t*)out, batch, seq, heads,
-                                                   flags, dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr, ld_mx);
+    const uint16_t* q = (const uint16_t*)qkv;
+    uint16_t* o = (uint16_t*)out;
+    uint8_t* mx = dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr;
+    if (dtype == AACLIP_F16) {
+      if (v == 2) launch_attn<true, 4, 2, 2>(q, o, batch, seq, heads, flags, nullptr, 0, s);
+      else launch_attn<true, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, nullptr, 0, s);
+    } else {
+      if (v == 2) launch_attn<false, 4, 2, 2>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
+      else launch_attn<false, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
+    }
   } else {
     dim3 grid(ceil_div(seq, 64), batch * heads);
     attn_f32_kernel<<<grid, 64, 0, s>>>((const float*)qkv, (float*)out, seq, heads, flags & AACLIP_ATTN_CAUSAL);

@@ -174,6 +174,10 @@ int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
  * e8m0 scale per (row, head) in out_mx [heads/2][ld_mx >= batch*seq][2] (the out-proj
  * A operand of aaclip_gemm_fp8mx, config C5); out_mx ignored otherwise. */
 
+/* Tuning hook for the 16-bit attention kernel: 0 = default, 1 = 4 waves x 32 queries per
+ * workgroup, 2 = 2 waves x 64 queries. Process-global; for benchmarking. */
+int aaclip_set_attn_variant(int variant);
+
 /*
  * Patchify for conv1-as-GEMM: img [batch, channels, S, S] fp32 ->
  * cols [batch*(S/patch)^2, k_padded], column k = c*patch*patch + kh*patch + kw

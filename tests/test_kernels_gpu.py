@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from aaclip import ops
+from aaclip import _lib, ops
 from oracle import aaclip_np as R
 
 pytestmark = pytest.mark.gpu
@@ -225,6 +225,24 @@ def test_attention_bf16(dev, B, N, H, causal):
     ref = _attn_ref(qkv, B, N, H, causal)
     err = (out.double() - ref).abs().max().item()
     assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (2, 73, 4, False),
+                                          (1, 200, 2, False)])
+def test_attention_variant_2x64(dev, dt, B, N, H, causal):
+    """aaclip_set_attn_variant(2): 2 waves x 64 queries, 2-stage ring (the benchmarked
+    alternative workgroup shape) against the same float64 reference."""
+    torch.manual_seed(B * N + 7)
+    qkv = (torch.randn(B * N, 3 * H * 64, device=dev) * 1.5).to(dt)
+    out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
+    _lib.call("aaclip_set_attn_variant", 2)
+    try:
+        ops.attention(qkv, out, B, N, H, causal=causal)
+    finally:
+        _lib.call("aaclip_set_attn_variant", 0)
+    err = (out.double() - _attn_ref(qkv, B, N, H, causal)).abs().max().item()
+    assert err < (3e-2 if dt == torch.bfloat16 else 4e-3), err
 
 
 @pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (3, 77, 12, True)])

@@ -5,7 +5,7 @@
 // (variants must agree to within bf16 rounding of the same math).
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iaa-clip_amd/csrc -DATTN_STAGES=3 \
-//         tools/attn_bench.hip -o /tmp/attn_s3 && /tmp/attn_s3
+//         tools/attn_bench.hip -o /tmp/attn_s3 && /tmp/attn_s3 [B] [N] [variant]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -17,6 +17,8 @@
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 32, N = argc > 2 ? atoi(argv[2]) : 577, H = 16, D = H * 64, reps = 50;
+  const int variant = argc > 3 ? atoi(argv[3]) : 0;  // aaclip_set_attn_variant
+  if (aaclip_set_attn_variant(variant)) return 3;
   const size_t nq = (size_t)B * N * 3 * D, no = (size_t)B * N * D;
   std::vector<uint16_t> h(nq);
   uint32_t x = 12345;
@@ -59,7 +61,7 @@ int main(int argc, char** argv) {
     cs += (double)f * (double)((i % 97) + 1);
   }
   const double flop = 4.0 * B * (double)N * N * D;
-  printf("stages=%d occ=%d  %8.2f us  %7.1f TFLOP/s  checksum %.6e\n", ATTN_STAGES, ATTN_OCC, best * 1e3,
+  printf("variant=%d N=%d  %8.2f us  %7.1f TFLOP/s  checksum %.6e\n", variant, N, best * 1e3,
          flop / (best * 1e-3) / 1e12, cs);
   return 0;
 }

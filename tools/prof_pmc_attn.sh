@@ -1,9 +1,9 @@
 #!/bin/bash
-# PMC passes over the standalone attention harness (tools/attn_bench.hip build):
-# wave-state split (parked / issue-stalled / active), LDS conflicts, MFMA busy.
-# usage: tools/prof_pmc_attn.sh OUTDIR BINARY
+# PMC passes over the attention kernel (tools/attn_variants.py --eager, one variant
+# and sequence length per run): wave-state split (parked / issue-stalled / active),
+# LDS conflicts, MFMA busy. usage: tools/prof_pmc_attn.sh OUTDIR VARIANT [SEQ]
 set -o pipefail
-OUT=$1; BIN=$2
+OUT=$1; VAR=$2; SEQ=${3:-577}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 groups=(
@@ -13,7 +13,9 @@ groups=(
 )
 i=0
 for g in "${groups[@]}"; do
-  timeout -k 10 120 rocprofv3 --pmc $g --output-format csv -d "$OUT/pmc$i" -o run -- "$BIN" > "$OUT/pmc$i.log" 2>&1 || { echo "pmc pass $i failed rc=$?"; tail -5 "$OUT/pmc$i.log"; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $g --output-format csv -d "$OUT/pmc$i" -o run -- \
+    python3 tools/attn_variants.py --eager 10 --seqs "$SEQ" --variants "$VAR" > "$OUT/pmc$i.log" 2>&1 \
+    || { echo "pmc pass $i failed rc=$?"; tail -5 "$OUT/pmc$i.log"; exit 1; }
   i=$((i+1))
 done
 echo "pmc ok"
