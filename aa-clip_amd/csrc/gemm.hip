@@ -108,6 +108,20 @@ __device__ __forceinline__ float gelu_fast(float v) {
   return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(w));
 }
 
+// gelu_fast on a column pair in packed f32 arithmetic (v_pk_mul/v_pk_fma/v_pk_add: two
+// elements per VALU issue; the epilogue runs with no MFMA beside it, so the packed
+// forms are pure savings here): 2 v_med3 + 5 packed + 2 v_exp + 2 v_rcp per pair,
+// the same roundings as gelu_fast element by element.
+__device__ __forceinline__ float2_t gelu_fast2(float2_t v) {
+  const float2_t vc = {__builtin_amdgcn_fmed3f(v[0], -8.0f, 8.0f), __builtin_amdgcn_fmed3f(v[1], -8.0f, 8.0f)};
+  const float2_t s = vc * vc;
+  const float2_t c2 = {0.0010142630f, 0.0010142630f}, c1 = {-0.10677572f, -0.10677572f},
+                 c0 = {-2.3011212f, -2.3011212f}, one = {1.0f, 1.0f};
+  const float2_t w = vc * __builtin_elementwise_fma(s, __builtin_elementwise_fma(s, c2, c1), c0);
+  const float2_t d = float2_t{__builtin_amdgcn_exp2f(w[0]), __builtin_amdgcn_exp2f(w[1])} + one;
+  return v * float2_t{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+}
+
 // Epilogue on one element C[m, n] (m < M checked by the caller).
 __device__ __forceinline__ void epilogue_store1(const GemmArgs& a, int m, int n, float v) {
   const int orow = remap_row(a, m);
@@ -210,9 +224,10 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
         v[j] = acc[i][j] * wsc[j] + bias[j];
       else
         v[j] = acc[i][j] + bias[j];
-      if (epi & AACLIP_EPI_GELU)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[j][t] = gelu_fast(v[j][t]);
+      if (epi & AACLIP_EPI_GELU) {
+        const float2_t lo = gelu_fast2(float2_t{v[j][0], v[j][1]}), hi = gelu_fast2(float2_t{v[j][2], v[j][3]});
+        v[j] = float4_t{lo[0], lo[1], hi[0], hi[1]};
+      }
       if (epi & AACLIP_EPI_LEAKY)
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[j][t] = v[j][t] >= 0.f ? v[j][t] : 0.01f * v[j][t];
