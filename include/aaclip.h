@@ -174,8 +174,9 @@ int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
  * e8m0 scale per (row, head) in out_mx [heads/2][ld_mx >= batch*seq][2] (the out-proj
  * A operand of aaclip_gemm_fp8mx, config C5); out_mx ignored otherwise. */
 
-/* Tuning hook for the 16-bit attention kernel: 0 = default, 1 = 4 waves x 32 queries per
- * workgroup, 2 = 2 waves x 64 queries. Process-global; for benchmarking. */
+/* Tuning hook for the 16-bit attention kernel: 0 = default (3), 1 = 4 waves x 32 queries per
+ * workgroup, 2 = 2 waves x 64 queries, 3 = 1 with each full key tile phase-split so one
+ * query block's softmax runs beside the other's MFMAs. Process-global; for benchmarking. */
 int aaclip_set_attn_variant(int variant);
 
 /*

@@ -227,16 +227,18 @@ def test_attention_bf16(dev, B, N, H, causal):
     assert err < 3e-2, err
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (2, 73, 4, False),
                                           (1, 200, 2, False)])
-def test_attention_variant_2x64(dev, dt, B, N, H, causal):
-    """aaclip_set_attn_variant(2): 2 waves x 64 queries, 2-stage ring (the benchmarked
-    alternative workgroup shape) against the same float64 reference."""
+def test_attention_variants(dev, variant, dt, B, N, H, causal):
+    """aaclip_set_attn_variant: 1 = the un-split full tile, 2 = 2 waves x 64 queries with a
+    2-stage ring (the benchmarked alternatives to the default) against the same float64
+    reference."""
     torch.manual_seed(B * N + 7)
     qkv = (torch.randn(B * N, 3 * H * 64, device=dev) * 1.5).to(dt)
     out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
-    _lib.call("aaclip_set_attn_variant", 2)
+    _lib.call("aaclip_set_attn_variant", variant)
     try:
         ops.attention(qkv, out, B, N, H, causal=causal)
     finally:
