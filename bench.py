@@ -447,6 +447,8 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the config-C5 leg (448 px, 6 levels, fp8)")
     ap.add_argument("--no-modes", action="store_true", help="skip the fp16 / fp32 mode throughput leg")
     ap.add_argument("--gemm-variant", type=int, default=0, help="aaclip_set_gemm_variant value (A/B runs)")
+    ap.add_argument("--dtype", choices=("bf16", "fp16"), default="bf16",
+                    help="compute dtype of the timed step (C2 is quoted in bf16; fp16 = the contract mode, for A/B)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -465,7 +467,7 @@ def main():
         from aaclip import _lib
         _lib.call("aaclip_set_gemm_variant", args.gemm_variant)
     vp, ad = synthetic_visual_weights(dev)
-    eng = VisualEngine(vp, ad, dtype=torch.bfloat16)
+    eng = VisualEngine(vp, ad, dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16)
     B, S = args.batch, args.img_size
     # one global batch of B * world images (the same seeded tensor on every rank);
     # each rank owns its shard_range slice (C3: 256 = 8 x 32), weights replicated
@@ -520,9 +522,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": args.dtype,
         "data": "synthetic (N(0,1) images on device, random-init ViT-L/14-336 + adapters)",
-        "config": {"workload": "C2: AA-CLIP anomaly-map inference, ViT-L/14-336, bf16, 4 levels, 2 anchors, "
+        "config": {"workload": f"C2: AA-CLIP anomaly-map inference, ViT-L/14-336, {args.dtype}, 4 levels, 2 anchors, "
                                "Industrial blur, per-GPU batch of images",
                    "global_batch": n_total, "img_size": S, "per_gpu_batch": B,
                    "parallelism": f"image-sharded dp{world} (shard_range slices of one global batch "
