@@ -32,12 +32,18 @@ __device__ __forceinline__ short4_t tr_read(const char* p) {
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
 // Cross-lane max over the 4 lanes {c, c+16, c+32, c+48} that hold one query's
-// scores: v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip).
+// scores: v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip). The two
+// combines are single v_max_f32 in asm: fmaxf's IEEE semantics make hipcc
+// canonicalise both permlane outputs first (2 extra v_max per combine); the inputs
+// here are finite scores or -inf. The s_nop covers the VALU-write -> permlane-read
+// hazard the compiler does not see through the asm.
 __device__ __forceinline__ float max_over_groups(float v) {
   auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+  float m;
+  asm("v_max_f32 %0, %1, %2\n\ts_nop 1" : "=v"(m) : "v"(a[0]), "v"(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(b[0]), "v"(b[1]));
+  return m;
 }
 
 // One 64-key tile for one wave: NKB live 16-key blocks (1, 2 or 4), NQB live
