@@ -151,6 +151,10 @@ def main():
         grid = torch.empty(P, device=dev)
         ms = timeit(lambda: ops.patch_scores(levels, T, grid), args.reps)
         res["patch_scores"] = (ms, (4 * P * 768 * 4 + P * 4) / ms / 1e6)
+        S = 14 * 24
+        amap = torch.empty(B, S, S, device=dev)  # both stages: patch scores + blur/upsample
+        ms = timeit(lambda: ops.anomaly_map(levels, T, amap, grid, g=24, ksize=7, sigma=1.0), args.reps)
+        res["anomaly_map"] = (ms, (4 * P * 768 * 4 + B * S * S * 4) / ms / 1e6)
     if args.only == "prep":  # device preprocessing: B decoded 1024x1024 RGB -> fp32 [B,3,S,S] (+ masks)
         from aaclip.preprocess import Preprocessor
         S = 336 if args.tokens == 577 else 448
@@ -169,7 +173,7 @@ def main():
         ms = timeit(lambda: ops.layernorm(x, lw, lb, h), args.reps)
         res["layernorm"] = (ms, (R * W * 6) / ms / 1e6)
     for k, (ms, rate) in res.items():
-        unit = "GB/s" if k in ("layernorm", "patch_scores") or k.endswith("quantA") or k[:4] in ("prep", "mask") \
+        unit = "GB/s" if k in ("layernorm", "patch_scores", "anomaly_map") or k.endswith("quantA") or k[:4] in ("prep", "mask") \
             else "TFLOP/s"
         print(f"{k:10s} {ms * 1e3:9.1f} us  {rate:8.1f} {unit}")
 

@@ -52,6 +52,7 @@ if __name__ == "__main__":
         grids = {696 * 512, 928 * 512, 876 * 512, 1168 * 512}
         gemm = [e for e in s if "gemm_bf16" in e["kernel"] and e["grid_size"] in grids and "hbm_bytes" in e]
         mp = [e for e in s if "patch_scores" in e["kernel"] and "hbm_bytes" in e]
+        bu = [e for e in s if "blur_upsample" in e["kernel"] and "hbm_bytes" in e]
         t = {"source": f"rocprofv3 --pmc passes (tools/prof_pmc.sh) summarised by tools/pmc_summary.py from {a.root}; "
                        "read = FETCH_SIZE*1024*2 (gfx950 half-count correction), write = WRITE_SIZE*1024"}
         if gemm:
@@ -59,8 +60,10 @@ if __name__ == "__main__":
                          "per_shape": {str(e["grid_size"] // 512): e["hbm_bytes"] for e in gemm},
                          "l2_hit_rate": sum(e.get("l2_hit_rate", 0) for e in gemm) / len(gemm),
                          "mfma_busy_frac": sum(e.get("mfma_busy_frac", 0) for e in gemm) / len(gemm)}
-        if mp:
-            t["map"] = {"bytes_per_launch": mp[0]["hbm_bytes"], "l2_hit_rate": mp[0].get("l2_hit_rate")}
+        if mp:  # the anomaly map as one operation: stage 1 (patch scores) + stage 2 (blur + upsample)
+            t["map"] = {"bytes_per_launch": mp[0]["hbm_bytes"] + (bu[0]["hbm_bytes"] if bu else 0),
+                        "stage1_bytes": mp[0]["hbm_bytes"], "stage2_bytes": bu[0]["hbm_bytes"] if bu else None,
+                        "l2_hit_rate": mp[0].get("l2_hit_rate")}
         open(a.traffic_out, "w").write(json.dumps(t, indent=1))
     txt = json.dumps(s, indent=1)
     if a.out:
