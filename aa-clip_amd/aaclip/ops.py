@@ -91,6 +91,12 @@ GEMM_FAMILIES = (3, 8, 1, 9, 2)
 _tuned = {}
 
 
+def pin_gemm(dtype: int, M: int, N: int, K: int, family: int) -> None:
+    """aaclip_gemm_pin: launch tile family `family` (GEMM_FAMILIES; 0 = back to the
+    per-shape heuristic) for every 16-bit GEMM of this (dtype tag, M, N, K)."""
+    call("aaclip_gemm_pin", dtype, M, N, K, family)
+
+
 def tune_gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, reps: int = 3, **epilogue) -> int:
     """Measure every tile family on these operands with this epilogue (HIP events on the
     current stream) and pin the fastest for the shape (aaclip_gemm_pin). The families

@@ -553,7 +553,16 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
 // Loads past the last K-step re-read its columns into regions nobody reads again,
 // so the vmcnt arithmetic stays uniform. Operands via buffer descriptors (rows >= M
 // read as zero; outputs dropped by the epilogue's bound check).
-template <bool H16>
+// PERSIST: one workgroup per CU walks tiles blockIdx.x, + gridDim.x, ... (same XCD:
+// the grid is a multiple of 8 or the whole tile set). The K-step index runs on
+// across tiles: the loads the last two K-steps of tile t would issue past its end
+// (the phantom loads) fetch tile t+1's K-steps 0-1 instead, so tile t+1 has no
+// prologue and its first regions land while tile t's epilogue runs. The epilogue's
+// S stores then sit in the in-order vmcnt stream between those DMAs and the next
+// ones: the four phases of tile t+1's first K-step wait vmcnt(8 + S) (S counted per
+// epilogue case; 0 = strict for edge tiles and the run-time-flag epilogues), so the
+// stores drain under four MFMA phases before vmcnt(8) requires them.
+template <bool H16, bool PERSIST>
 __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   using V8 = h16x8_t<H16>;
   constexpr int BM = 256, BN = 256, TM = 128, TN = 64, RM = 8, RN = 4;
@@ -565,9 +574,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
-  int tm, tn;
-  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int ntiles = a.tiles_m * a.tiles_n;
   const auto ars = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)((uint32_t)a.M * (uint32_t)a.lda * 2u),
                                                      0x00020000);
   const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, (int)((uint32_t)a.N * (uint32_t)a.ldw * 2u),
@@ -576,21 +583,30 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   // logical chunk (t%8) ^ (row%8) (row%8 = (t/8)%8 in every piece)
   const int prow = t >> 3;
   const int pchunk = ((t & 7) ^ (prow & 7)) * 8;
-  const int a_vo = ((m0 + prow) * (int)a.lda + pchunk) * 2;
-  const int w_vo = ((n0 + ((prow >> 5) & 1) * 64 + (prow & 31)) * (int)a.ldw + pchunk) * 2;
+  auto a_vo_of = [&](int m0) { return ((m0 + prow) * (int)a.lda + pchunk) * 2; };
+  auto w_vo_of = [&](int n0) { return ((n0 + ((prow >> 5) & 1) * 64 + (prow & 31)) * (int)a.ldw + pchunk) * 2; };
   const int a_row = (int)a.lda * 2, w_row = (int)a.ldw * 2;  // bytes per row
   const int nk = a.K / 64;
-  // region r of K-step kt into stage kt&1 (r: 0 = A0, 1 = A1, 2 = B0, 3 = B1)
+  int tile = blockIdx.x;
+  int tm, tn;
+  tile_coords(tile, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
+  int a_vo = a_vo_of(tm * BM), w_vo = w_vo_of(tn * BN);
+  int a_vo_next = a_vo, w_vo_next = w_vo;  // the next tile's, when there is one
+  bool has_next = false;
+  // region r of K-step kt into stage kt&1 (r: 0 = A0, 1 = A1, 2 = B0, 3 = B1); kt >= nk
+  // is the next tile's K-step kt - nk (PERSIST) or a phantom re-read of the last one
   auto issue = [&](int r, int kt) {
-    const int kc = min(kt, nk - 1) * 128;  // phantom loads past the end re-read the last K-step
+    const bool nxt = PERSIST && kt >= nk && has_next;
+    const int kc = (nxt ? kt - nk : min(kt, nk - 1)) * 128;
+    const int avo = nxt ? a_vo_next : a_vo, wvo = nxt ? w_vo_next : w_vo;
     char* dst = smem + (kt & 1) * STAGE + r * REGION;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       if (r < 2)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, LDS_PTR(dst + g * 8192 + wid * 1024), 16, a_vo,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, LDS_PTR(dst + g * 8192 + wid * 1024), 16, avo,
                                                  (g * 128 + r * 64) * a_row + kc, 0, 0);
       else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + g * 8192 + wid * 1024), 16, w_vo,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + g * 8192 + wid * 1024), 16, wvo,
                                                  (g * 128 + (r - 2) * 32) * w_row + kc, 0, 0);
     }
   };
@@ -604,10 +620,6 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
     b_rd[kk] = 2 * REGION + (wc * 32 + fr) * 128 + sw;
   }
   float4_t acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
   V8 af[4][2], bfr[2][2][2];  // A sub-block (4 tiles x kk), B sub-blocks [q][j][kk]
 
   // prologue: all of K-step 0, then A0 / B0 of K-step 1 (the steady state's P3/P4 of K-step -1)
@@ -645,8 +657,19 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       for (int kk = 0; kk < 2; ++kk)
         bfr[q][j][kk] = *(const V8*)(st + q * REGION + b_rd[kk] + j * 2048);
   };
-#define PH_SYNC_MFMA(QA, QB)                                 \
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");           \
+  // phase-end wait: vmcnt(8), or vmcnt(8 + S) in the first K-step after an epilogue of S stores
+  auto ph_wait = [&](int S) {
+    if (!PERSIST || S == 0)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (S == 16)
+      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (S == 32)
+      asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(56)" ::: "memory");
+  };
+#define PH_SYNC_MFMA(QA, QB, S)                              \
+  ph_wait(S);                                                \
   __builtin_amdgcn_s_barrier();                              \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
   __builtin_amdgcn_sched_barrier(0);                         \
@@ -654,53 +677,85 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   __builtin_amdgcn_sched_barrier(0);                         \
   __builtin_amdgcn_s_barrier();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* st = smem + (kt & 1) * STAGE;
-    // P1: A0 x B0
-    read_b(st, 0);
-    read_a(st, 0);
-    issue(3, kt + 1);
-    PH_SYNC_MFMA(0, 0)
-    // P2: A0 x B1
-    read_b(st, 1);
-    issue(1, kt + 1);
-    PH_SYNC_MFMA(0, 1)
-    // P3: A1 x B1
-    read_a(st, 1);
-    issue(0, kt + 2);
-    PH_SYNC_MFMA(1, 1)
-    // P4: A1 x B0
-    issue(2, kt + 2);
-    PH_SYNC_MFMA(1, 0)
-  }
-#undef PH_SYNC_MFMA
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phantom loads drained before exit
-  if (wr == 0) __builtin_amdgcn_s_barrier();         // re-balance the stagger
-  if (a.dbg & 1) {
+  const bool bf16_out = a.out_dtype != AACLIP_F32;
+  const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
+  int s_prev = 0;  // stores the previous tile's epilogue left in the vmcnt stream (0 = none / unknown)
+  for (;;) {
+    const int m0 = tm * BM, n0 = tn * BN;
+    int tm_n = 0, tn_n = 0;
+    if constexpr (PERSIST) {
+      has_next = tile + (int)gridDim.x < ntiles;
+      if (has_next) {
+        tile_coords(tile + (int)gridDim.x, a.tiles_m, a.tiles_n, tm_n, tn_n, a.group_m);
+        a_vo_next = a_vo_of(tm_n * BM);
+        w_vo_next = w_vo_of(tn_n * BN);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
-      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-  const int mw = m0 + wr * TM, nw = n0 + wc * TN;
-  const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
-  const bool bf16_out = a.out_dtype != AACLIP_F32;
-#define EPI_CASE(BF, E)                                                 \
-  if (bf16_out == (BF) && key == (E)) {                                 \
-    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane); \
-    return;                                                             \
-  }
-  EPI_CASE(true, AACLIP_EPI_BIAS)
-  EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)
-  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)
-  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)
-  EPI_CASE(false, AACLIP_EPI_LEAKY)
+      for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* st = smem + (kt & 1) * STAGE;
+      const int S = kt == 0 ? s_prev : 0;
+      // P1: A0 x B0
+      read_b(st, 0);
+      read_a(st, 0);
+      issue(3, kt + 1);
+      PH_SYNC_MFMA(0, 0, S)
+      // P2: A0 x B1
+      read_b(st, 1);
+      issue(1, kt + 1);
+      PH_SYNC_MFMA(0, 1, S)
+      // P3: A1 x B1
+      read_a(st, 1);
+      issue(0, kt + 2);
+      PH_SYNC_MFMA(1, 1, S)
+      // P4: A1 x B0
+      issue(2, kt + 2);
+      PH_SYNC_MFMA(1, 0, S)
+    }
+    // both wave rows run the epilogue together (row 0 waits out row 1's last phase);
+    // row 1 re-takes its one-barrier lag before the next tile
+    if (wr == 0) __builtin_amdgcn_s_barrier();
+    const int mw = m0 + wr * TM, nw = n0 + wc * TN;
+    // S for the next tile's first K-step: a LOWER bound on the VMEM ops this epilogue
+    // issues between the next tile's prefetched regions and its own next DMA (stores;
+    // the bias / residual loads only add to it). Edge tiles skip whole row groups: 0.
+    const bool full = m0 + BM <= a.M;
+    s_prev = 0;
+    if (a.dbg & 1) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else {
+#define EPI_CASE(BF, E, NS)                                               \
+  if (bf16_out == (BF) && key == (E)) {                                   \
+    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane);   \
+    s_prev = full && !(a.dbg & 2) ? (NS) : 0;                             \
+  } else
+      EPI_CASE(true, AACLIP_EPI_BIAS, RM * RN / 2)
+      EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU, RM * RN / 2)
+      EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID, RM * RN)
+      EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16, RM * RN + RM * RN / 2)
+      EPI_CASE(false, AACLIP_EPI_LEAKY, RM * RN)
 #undef EPI_CASE
-  if (bf16_out)
-    wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane);
-  else
-    wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane);
+      if (bf16_out)
+        wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane);
+      else
+        wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane);
+    }
+    if (!PERSIST || !has_next) break;
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+    tile += gridDim.x;
+    tm = tm_n;
+    tn = tn_n;
+    a_vo = a_vo_next;
+    w_vo = w_vo_next;
+  }
+#undef PH_SYNC_MFMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phantom loads drained before exit
 }
 
 // ============================ 8-phase ping-pong fp8 MX kernel (256x256, K-step 128)
@@ -885,15 +940,22 @@ int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
   return AACLIP_OK;
 }
 
-template <bool H16>
+int cu_count();
+
+template <bool H16, bool PERSIST = false>
 int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   if (a.N % 256 || a.K % 64) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
+  const int tiles = a.tiles_m * a.tiles_n;
+  // persistent: one workgroup per CU, a multiple of 8 so each keeps its XCD's tile run;
+  // the K-step stream across tiles needs an even K-step count (stage = kt & 1)
+  const int cus = cu_count() & ~7;
+  if (PERSIST && !((a.K / 64) % 2 == 0 && tiles > cus && cus > 0)) return launch_bf16_8ph<H16, false>(a, s);
   const size_t lds = 2 * 4 * 128 * 128;
   static unsigned attr_dev = 0;
-  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16>, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
-  gemm_bf16_8ph_kernel<H16><<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
+  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, PERSIST>, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
+  gemm_bf16_8ph_kernel<H16, PERSIST><<<PERSIST ? cus : tiles, 512, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -973,6 +1035,9 @@ int dispatch16(GemmArgs a, hipStream_t s) {
     case 4:  // 8-phase for the wide GEMMs only (N >= 2048), 320x256 below
       if (N % 256 == 0 && (fam == 3 || N >= 2048) && fits) return launch_bf16_8ph<H16>(a, s);
       break;
+    case 5:  // A/B: the persistent 8-phase kernel wherever N % 256 == 0
+      if (N % 256 == 0 && fits) return launch_bf16_8ph<H16, true>(a, s);
+      break;
     case 9: return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);  // 128x128 everywhere (A/B)
     case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
       if (N % 256 == 0) return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
@@ -1009,6 +1074,9 @@ extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
     case 4:
       if (N % 256 == 0 && (fam == 3 || N >= 2048)) return "gemm_bf16_8ph_kernel<256,256>";
       break;
+    case 5:
+      if (N % 256 == 0) return "gemm_bf16_8ph_kernel<256,256,persistent>";
+      break;
     case 8:
       if (N % 256 == 0) return "gemm_bf16_kernel<320,256,2,4>";
       break;
@@ -1040,11 +1108,12 @@ extern "C" int aaclip_gemm_pin(int in_dtype, int M, int N, int K, int family) {
 
 extern "C" int aaclip_set_gemm_variant(int variant) {
   // bits 0-3: tile family (0 default = per-shape choice, 1 = 256x256, 2 = 256x128, 3/4 = 256x256
-  // 8-phase ping-pong everywhere / for N >= 2048, 6 = MX fp8 on the 256x256 LDS-DMA kernel instead
+  // 8-phase ping-pong everywhere / for N >= 2048, 5 = persistent 8-phase, 6 = MX fp8 on the
+  // 256x256 LDS-DMA kernel instead
   // of its 8-phase default, 8 = 320x256 everywhere); bits 4-7: tile-order
   // group height (0 = 8); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 2048 || fam > 9 || fam == 5 || fam == 7) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 2048 || fam > 9 || fam == 7) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 8;
   g_setprio = (variant >> 8) & 1;

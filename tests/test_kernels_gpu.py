@@ -31,14 +31,14 @@ def test_gemm_bf16_plain(dev, M, N, K):
     assert err < 1e-3 * ref.abs().max().item() + 1e-4, err
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 8, 9])
+@pytest.mark.parametrize("variant", [1, 2, 3, 5, 8, 9])
 @pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (2000, 256, 64),
                                    (18464, 3072, 1024), (577 * 40, 1024, 512), (300, 512, 128)])
 def test_gemm_bf16_variants(dev, variant, M, N, K):
     """Forced bf16 tile families (256x256, 256x128, 256x256 8-phase ping-pong, 320x256);
     the default picks between the last two per shape and is covered by every other GEMM test."""
     from aaclip import _lib
-    if variant in (1, 3, 8) and N % 256:
+    if variant in (1, 3, 5, 8) and N % 256:
         pytest.skip("256x256 tile needs N % 256 == 0")
     torch.manual_seed(M * 7 + N)
     a = torch.randn(M, K, device=dev).bfloat16()
@@ -75,8 +75,9 @@ def test_gemm_bf16_out_epilogue(dev, gelu, M, N):
     assert (err <= 8e-3 * ref.abs() + 2e-3).all(), err.max().item()
 
 
-@pytest.mark.parametrize("M,N,K", [(18464, 4096, 1024), (4100, 3072, 4096), (513, 256, 192)])
-def test_gemm_8phase_race_screen(dev, M, N, K):
+@pytest.mark.parametrize("variant", [3, 5])
+@pytest.mark.parametrize("M,N,K", [(18464, 4096, 1024), (4100, 3072, 4096), (513, 256, 192), (9232, 1024, 4096)])
+def test_gemm_8phase_race_screen(dev, variant, M, N, K):
     """The 8-phase kernel's LDS hand-offs are placed by vmcnt/barrier counting: a read
     placed too early passes whenever the DMA happens to land first, so screen many
     launches for run-to-run differences (bit-identical expected) and check one
@@ -86,7 +87,7 @@ def test_gemm_8phase_race_screen(dev, M, N, K):
     a = torch.randn(M, K, device=dev).bfloat16()
     w = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
     outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(2)]
-    _lib.call("aaclip_set_gemm_variant", 3)
+    _lib.call("aaclip_set_gemm_variant", variant)
     try:
         ops.gemm(a, w, outs[0])
         ref = a.double() @ w.double().T
@@ -108,7 +109,7 @@ def test_gemm_bf16_asymmetric_identity(dev):
     torch.testing.assert_close(out, w.float().T, atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 8, 9])
 def test_gemm_epilogues_bf16(dev, variant):
     from aaclip import _lib
     _lib.call("aaclip_set_gemm_variant", variant)

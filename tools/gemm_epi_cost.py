@@ -36,7 +36,8 @@ def main():
             fl = 2.0 * M * N * K
             res = []
             for rnd in range(2):
-                for tag, v in (("default", 0), (f"fam{fam}", fam), ("no-stores", fam | 1024), ("no-epilogue", fam | 512)):
+                for tag, v in (("default", 0), (f"fam{fam}", fam), ("fam3", 3), ("persist", 5), ("no-stores", fam | 1024),
+                               ("no-epilogue", fam | 512)):
                     _lib.call("aaclip_set_gemm_variant", v)
                     t = graph_time(call, reps=20)
                     if rnd:
