@@ -447,6 +447,7 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the config-C5 leg (448 px, 6 levels, fp8)")
     ap.add_argument("--no-modes", action="store_true", help="skip the fp16 / fp32 mode throughput leg")
     ap.add_argument("--gemm-variant", type=int, default=0, help="aaclip_set_gemm_variant value (A/B runs)")
+    ap.add_argument("--attn-variant", type=int, default=0, help="aaclip_set_attn_variant value (A/B runs)")
     ap.add_argument("--dtype", choices=("bf16", "fp16"), default="bf16",
                     help="compute dtype of the timed step (C2 is quoted in bf16; fp16 = the contract mode, for A/B)")
     args = ap.parse_args()
@@ -463,9 +464,10 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    if args.gemm_variant:
+    if args.gemm_variant or args.attn_variant:
         from aaclip import _lib
         _lib.call("aaclip_set_gemm_variant", args.gemm_variant)
+        _lib.call("aaclip_set_attn_variant", args.attn_variant)
     vp, ad = synthetic_visual_weights(dev)
     eng = VisualEngine(vp, ad, dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16)
     B, S = args.batch, args.img_size
