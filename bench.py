@@ -432,6 +432,11 @@ def modes_leg(vp, ad, x, T, steps: int, warmup: int, streams: int):
     return out
 
 
+def _streams_arg(v: str):
+    """--streams N (equal chunks) or an explicit chunk-size list 'a,b,...' (summing to --batch)."""
+    return tuple(int(t) for t in v.split(",")) if "," in v else int(v)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -442,7 +447,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="steady-state seconds per CPU-baseline leg (0 = skip the CPU leg and parity)")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--streams", type=int, default=2, help="concurrent image chunks per GPU (HIP streams)")
+    ap.add_argument("--streams", type=_streams_arg, default=2,
+                    help="concurrent image chunks per GPU (HIP streams); 'a,b,...' = explicit chunk sizes")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-C5 leg (448 px, 6 levels, fp8)")
     ap.add_argument("--no-modes", action="store_true", help="skip the fp16 / fp32 mode throughput leg")
@@ -452,6 +458,7 @@ def main():
                     help="compute dtype of the timed step (C2 is quoted in bf16; fp16 = the contract mode, for A/B)")
     args = ap.parse_args()
 
+    n_streams = args.streams if isinstance(args.streams, int) else len(args.streams)  # for the other legs
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -544,13 +551,13 @@ def main():
         run = None
         line["modes"] = modes_leg(vp, ad, x, T, args.steps, args.warmup, args.streams)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(dev, args.streams, args.cpu_seconds)
+        line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(dev, n_streams, args.cpu_seconds)
     if rank == 0 and world == 1 and not args.no_roofline:
         line["preprocess"] = preprocess_leg(dev, B, S)
     if rank == 0 and world == 1 and not args.no_c5:
         del eng, run, vp, ad
         torch.cuda.empty_cache()
-        line["c5"] = c5_leg(dev, max(3, args.steps // 2), args.warmup, args.streams)
+        line["c5"] = c5_leg(dev, max(3, args.steps // 2), args.warmup, n_streams)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
