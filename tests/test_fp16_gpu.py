@@ -204,3 +204,21 @@ def test_f16_batch_composition_invariance(dev, weights):
     for streams in (1, 2, (1, 4)):
         m, _ = eng.predict(x, T, "Industrial", streams=streams)
         assert torch.equal(m, ref), streams
+
+
+def test_concurrent_chunk_pins(dev, weights):
+    """Two 16-image chunks on two streams pin the 8-phase GEMM for their wide block
+    shapes while they are enqueued (VisualEngine._concurrent_pins): the maps and scores
+    are bit-identical to one stream (same K order), and the heuristic is back afterwards."""
+    from aaclip import _lib
+    eng = VisualEngine(*weights, dtype=H16)
+    g = torch.Generator(device=dev).manual_seed(5)
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
+    x = torch.randn(32, 3, 336, 336, device=dev, generator=g)
+    M = 16 * 577
+    plan = lambda: _lib.lib().aaclip_gemm_plan(_lib.F16, M, 4096, 1024).decode()  # noqa: E731
+    before = plan()
+    m1, s1 = (t.clone() for t in eng.predict(x, T, "Industrial", streams=1))
+    m2, s2 = eng.predict(x, T, "Industrial", streams=2)
+    assert torch.equal(m1, m2) and torch.equal(s1, s2)
+    assert plan() == before
