@@ -48,11 +48,12 @@ def _device_batch(input_data, prep, device):
 
 
 def get_predictions(model, class_text_embeddings, test_loader, device, img_size, dataset="MVTec", prep=None,
-                    n_total=None):
+                    n_total=None, streams=1):
     """test.py:53-99. With n_total (sharded run: test_loader holds this rank's
     shard_range slice of a class's n_total images) the per-image results of all
     ranks are all-gathered in shard order, so the return value is the whole class's
-    on every rank."""
+    on every rank. streams: concurrent image chunks per batch (HIP streams) for batches
+    of at least 8 images per chunk; per-image results do not depend on it."""
     masks, labels, preds, preds_image, file_names = [], [], [], [], []
     for input_data in test_loader:
         if prep is not None:
@@ -64,7 +65,8 @@ def get_predictions(model, class_text_embeddings, test_loader, device, img_size,
         masks.append(mask.cpu().numpy())
         labels.append(np.asarray(input_data["label"]))
         file_names.extend(input_data["file_name"])
-        pmap, score = model.predict(image, class_text_embeddings, DOMAINS[dataset])
+        nst = streams if image.shape[0] >= 8 * streams else 1
+        pmap, score = model.predict(image, class_text_embeddings, DOMAINS[dataset], streams=nst)
         preds.append(pmap.clone())
         preds_image.append(score.clone())
     # maps and scores stay on the device: metrics_eval ranks them there
@@ -105,6 +107,9 @@ def parse_args(argv=None):
     parser.add_argument("--compute_dtype", type=str, default="fp16", choices=["bf16", "fp16", "fp32", "fp8"],
                         help="visual tower MFMA dtype: fp16 (default; meets the map-parity contract at the bf16 "
                              "rate), bf16, fp32 (fp32-MFMA parity mode) or fp8 (config C5)")
+    parser.add_argument("--streams", type=int, default=2,
+                        help="concurrent image chunks per batch on HIP streams (bit-identical results; "
+                             "batches under 8 images per chunk run as one)")
     parser.add_argument("--gpu_preprocess", action="store_true",
                         help="decode on the host, resize + normalise on the GPU (bit-exact with the Pillow path)")
     return parser.parse_args(argv)
@@ -199,7 +204,8 @@ def run(args):
             with torch.no_grad():
                 masks, labels, preds, preds_image, file_names = get_predictions(
                     model=model, class_text_embeddings=text_embeddings[class_name], test_loader=loader,
-                    device=device, img_size=args.img_size, dataset=args.dataset, prep=prep, n_total=n_total)
+                    device=device, img_size=args.img_size, dataset=args.dataset, prep=prep, n_total=n_total,
+                    streams=args.streams)
             if args.visualize and rank == 0:
                 visualize(masks, preds.cpu().numpy(), file_names, args.save_path, args.dataset, class_name=class_name)
             result = metrics_eval(masks, labels, preds, preds_image, class_name, domain=DOMAINS[args.dataset])
