@@ -160,12 +160,12 @@ __global__ __launch_bounds__(NT) void bicubic_normalize_kernel(PrepArgs a) {
 }
 
 // ---- two-pass path (default when the caller passes a workspace): full-occupancy
-// passes with no per-tile row overlap. B=32 1024^2 -> 336: H 91 us + V 33 us
-// (single tiled kernel: 152 us). H is VALU-bound (16 unpredicated taps x 3
-// channels of byte * int32 MACs per output; 4-byte LDS reads + v_alignbyte
-// instead of byte reads measured the same). Pass H resamples every source row into the
-// uint8 intermediate image tmp [B][in_h][S][3] (Pillow's clipped intermediate);
-// pass V runs the vertical taps out of tmp (L2-resident rows, each read by ~ky/scale
+// passes with no per-tile row overlap. B=32 1024^2 -> 336 (profiles/r02/preprocess.txt):
+// H 51 us + V 18 us (round 1: 91 + 33; single tiled kernel: 152 us). H is VALU-bound
+// (14 tap slots x 3 channels of byte * weight MACs per output, as SDWA byte-select
+// v_mul_i32_i24 + v_add3). Pass H resamples every source row into the uint8
+// intermediate image tmp [B][in_h][S][3] (Pillow's clipped intermediate); pass V
+// runs the vertical taps out of tmp (L2-resident rows, each read by ~ky/scale
 // output rows) and writes the normalised CHW fp32 output.
 struct HArgs {
   const uint8_t* src;
@@ -180,10 +180,18 @@ constexpr int HK = 16;  // max taps held in registers by the horizontal pass (kx
 
 // blockDim = 64 * ceil(S / 64): thread x owns output column x, its taps live in
 // registers for all the workgroup's rows; the rows are staged in LDS by aligned
-// dword loads (8 in flight per thread) and read back as bytes.
-// K taps per column, unpredicated: the plan zero-fills taps past each column's
-// count (and srow carries K*3 spare bytes), so the short columns add 0 * byte
-// instead of branching per tap (a per-lane `t < n` test serialised the LDS reads).
+// 16-byte loads (all of a thread's loads in flight) and read back as aligned dwords.
+// K tap slots per column (tap_slots), unpredicated: the plan zero-fills taps past
+// each column's count (and srow carries 3*HK spare bytes), so the short columns add
+// 0 * byte instead of branching per tap (a per-lane `t < n` test serialised the LDS reads).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 24-bit signed view of a tap weight. Pillow's 8-bit weights are round(v * 2^22)
+// with |v| < 2 (normalised cubic taps), so the value is unchanged, and the
+// compiler can then use the full-rate v_mad_i32_i24 for byte * weight instead of
+// the quarter-rate 32-bit v_mul_lo_u32 (the product fits 31 bits either way).
+__device__ __forceinline__ int tap24(int w) { return (w << 8) >> 8; }
+
 template <int K>
 __global__ __launch_bounds__(1024) void resample_h_kernel(HArgs a) {
   const int nt = blockDim.x;
@@ -191,29 +199,38 @@ __global__ __launch_bounds__(1024) void resample_h_kernel(HArgs a) {
   const int b = blockIdx.y;
   const int r0 = blockIdx.x * a.rows, nr = min(a.rows, a.in_h - r0);
   const uint8_t* img = a.src + (size_t)b * a.img_stride;
-  const int ndw = (a.in_w * 3 + 3 + 3) >> 2;
-  constexpr int U = 8;
-  const int total = nr * ndw;
-  for (int i0 = threadIdx.x; i0 < total; i0 += nt * U) {
-    uint32_t v[U];
+  // staging: 16-byte aligned quads (an aligned quad holding a byte of the row never
+  // crosses a page: no fault past the end), all of a thread's loads in flight
+  // before its LDS writes. (row, quad) advances by nt without a per-load division.
+  const int nq = (a.in_w * 3 + 15 + 15) >> 4;  // quads per row incl. the <= 15-byte alignment shift
+  constexpr int U = 4;
+  int r = threadIdx.x / nq, q = threadIdx.x - r * nq;
+  const int rstep = nt / nq, qstep = nt - rstep * nq;
+  while (r < nr) {
+    u32x4 v[U];
     int dst[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * nt;
-      dst[u] = -1;
-      if (i < total) {
-        const int r = i / ndw, d = i - r * ndw;
-        const uintptr_t row = (uintptr_t)(img + (size_t)(r0 + r) * a.pitch);
-        const uintptr_t base = row & ~(uintptr_t)3;  // aligned dwords never cross a page
-        if ((int)(row - base) + a.in_w * 3 > d * 4) {
-          v[u] = *(const uint32_t*)(base + 4 * (uintptr_t)d);
-          dst[u] = r * a.srow + 4 * d;
-        }
+      // unconditional load (a past-the-end slot re-reads the row's first quad) so the
+      // compiler issues all U loads back to back; only the LDS store is predicated
+      const int rr = min(r, nr - 1);
+      const uint8_t* row = img + (size_t)(r0 + rr) * a.pitch;
+      const int mis = (int)((uintptr_t)row & 15);
+      const bool ok = r < nr && 16 * q < mis + a.in_w * 3;
+      v[u] = *(const u32x4*)(row - mis + (ok ? 16 * q : 0));
+      dst[u] = ok ? rr * a.srow + 16 * q : -1;
+      r += rstep;
+      q += qstep;
+      if (q >= nq) {
+        q -= nq;
+        ++r;
       }
     }
 #pragma unroll
+    for (int u = 0; u < U; ++u) asm volatile("" : "+v"(v[u]));  // keep every load ahead of the stores
+#pragma unroll
     for (int u = 0; u < U; ++u)
-      if (dst[u] >= 0) *(uint32_t*)(rows + dst[u]) = v[u];
+      if (dst[u] >= 0) *(u32x4*)(rows + dst[u]) = v[u];
   }
   __syncthreads();
   const int x = threadIdx.x;
@@ -221,16 +238,32 @@ __global__ __launch_bounds__(1024) void resample_h_kernel(HArgs a) {
     const int xmin = a.xb[2 * x];
     int w[K];
 #pragma unroll
-    for (int t = 0; t < K; ++t) w[t] = t < a.kx ? a.xk[(size_t)x * a.kx + t] : 0;  // kx is uniform
+    for (int t = 0; t < K; ++t) {  // clamped unconditional loads (all in flight), zero past kx (uniform)
+      const int wt = tap24(a.xk[(size_t)x * a.kx + min(t, a.kx - 1)]);
+      w[t] = t < a.kx ? wt : 0;
+    }
+    // the column's 3K-byte tap window starts at an arbitrary byte: read the dwords
+    // covering it at dword-aligned addresses and realign with v_alignbyte (byte-
+    // misaligned wide LDS reads measured ~33 LDS cycles per instruction: the pass
+    // was LDS-bound), then the byte picks below are compile-time (SDWA operands)
+    constexpr int NW = (3 * K + 3) / 4;  // window dwords
     for (int r = 0; r < nr; ++r) {
       const uintptr_t row = (uintptr_t)(img + (size_t)(r0 + r) * a.pitch);
-      const uint8_t* p = rows + r * a.srow + (int)(row & 3) + xmin * 3;
+      const int off = r * a.srow + (int)(row & 15) + xmin * 3;
+      const uint32_t* pd = (const uint32_t*)(rows + (off & ~3));
+      const uint32_t sh = (uint32_t)(off & 3);
+      uint32_t dw[NW + 1], win[NW];
+#pragma unroll
+      for (int j = 0; j <= NW; ++j) dw[j] = pd[j];
+#pragma unroll
+      for (int j = 0; j < NW; ++j) win[j] = __builtin_amdgcn_alignbyte(dw[j + 1], dw[j], sh);
+      auto byte = [&](int i) { return (int)((win[i >> 2] >> (8 * (i & 3))) & 255); };
       int s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
 #pragma unroll
       for (int t = 0; t < K; ++t) {
-        s0 += (int)p[3 * t + 0] * w[t];
-        s1 += (int)p[3 * t + 1] * w[t];
-        s2 += (int)p[3 * t + 2] * w[t];
+        s0 += byte(3 * t + 0) * w[t];
+        s1 += byte(3 * t + 1) * w[t];
+        s2 += byte(3 * t + 2) * w[t];
       }
       uint8_t* d = a.tmp + ((size_t)b * a.in_h + r0 + r) * a.tstride + x * 3;
       d[0] = (uint8_t)clip8(s0);
@@ -241,41 +274,92 @@ __global__ __launch_bounds__(1024) void resample_h_kernel(HArgs a) {
 }
 
 // one thread = 4 consecutive output pixels (12 intermediate bytes = 3 aligned
-// dwords per tap) of one output row; a 64-thread block covers 256 pixels and the
-// row's taps are block-uniform (scalar loads)
-__global__ __launch_bounds__(64) void resample_v_kernel(const uint8_t* __restrict__ tmp, int in_h, int S,
-                                                        int tstride, const int32_t* __restrict__ yb,
-                                                        const int32_t* __restrict__ yk, int ky, float m0,
-                                                        float m1, float m2, float s0_, float s1_, float s2_,
-                                                        float* __restrict__ out) {
-  const int b = blockIdx.z, y = blockIdx.y, x0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-  const int ymin = yb[2 * y], n = yb[2 * y + 1];
+// dwords per tap) of one output row; the (row, pixel-quad) pairs of an image are
+// numbered consecutively over 256-thread blocks, so every lane has work (a block
+// per output row left a third of the lanes idle at S = 336).
+// K > 0: K unpredicated taps, every tap row's loads in flight at once (the plan
+// zero-fills taps past each row's count; rows past the image are clamped, their
+// weight is 0). K == 0: the row's own tap count, a loop (ky > 16 downscales).
+struct VArgs {
+  const uint8_t* tmp;
+  int in_h, S, tstride;
+  const int32_t *yb, *yk;
+  int ky;
+  float mean[3], stdv[3];
+  float* out;
+};
+
+template <int K>
+__global__ __launch_bounds__(256) void resample_v_kernel(VArgs a) {
+  const uint8_t* __restrict__ tmp = a.tmp;
+  const int in_h = a.in_h, S = a.S, tstride = a.tstride, ky = a.ky;
+  const int32_t* __restrict__ yb = a.yb;
+  const int32_t* __restrict__ yk = a.yk;
+  float* __restrict__ out = a.out;
+  const int q4 = (S + 3) >> 2;
+  const int i = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  const int y = i / q4, x0 = (i - y * q4) * 4;
+  // normalisation table: lut[c][v] = (v / 255 - mean[c]) / std[c], the same IEEE
+  // expression per entry, so a lookup equals computing it per pixel (3 x 256 entries
+  // per block instead of 2 divisions for each of a thread's 12 outputs)
+  __shared__ float lut[3][256];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) lut[c][threadIdx.x] = ((float)threadIdx.x / 255.0f - a.mean[c]) / a.stdv[c];
+  __syncthreads();
+  if (y >= S) return;
+  const int ymin = yb[2 * y];
   const int32_t* k = yk + (size_t)y * ky;
-  if (x0 >= S) return;
-  const uint8_t* col = tmp + ((size_t)b * in_h + ymin) * tstride + x0 * 3;
+  const uint8_t* col = tmp + (size_t)b * in_h * tstride + x0 * 3;  // x0*3 % 12 == 0, tstride % 16 == 0
   int acc[12];
 #pragma unroll
   for (int e = 0; e < 12; ++e) acc[e] = 1 << (PREC - 1);
-#pragma unroll 2
-  for (int t = 0; t < n; ++t) {
-    const int w = k[t];
-    const uint32_t* q = (const uint32_t*)(col + (size_t)t * tstride);  // x0*3 % 12 == 0, tstride % 16 == 0
-    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+  auto tap = [&](uint32_t d0, uint32_t d1, uint32_t d2, int w) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       acc[e] += (int)((d0 >> (8 * e)) & 255) * w;
       acc[4 + e] += (int)((d1 >> (8 * e)) & 255) * w;
       acc[8 + e] += (int)((d2 >> (8 * e)) & 255) * w;
     }
+  };
+  if constexpr (K > 0) {
+    int w[K];
+    uint32_t d[K][3];
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int wt = tap24(k[min(t, ky - 1)]);
+      w[t] = t < ky ? wt : 0;
+      const uint32_t* q = (const uint32_t*)(col + (size_t)min(ymin + t, in_h - 1) * tstride);
+      d[t][0] = q[0];
+      d[t][1] = q[1];
+      d[t][2] = q[2];
+    }
+#pragma unroll
+    for (int t = 0; t < K; ++t) tap(d[t][0], d[t][1], d[t][2], w[t]);
+  } else {
+    const int n = yb[2 * y + 1];
+#pragma unroll 2
+    for (int t = 0; t < n; ++t) {
+      const uint32_t* q = (const uint32_t*)(col + (size_t)(ymin + t) * tstride);
+      tap(q[0], q[1], q[2], tap24(k[t]));
+    }
   }
   const size_t plane = (size_t)S * S, o = (size_t)b * 3 * plane + (size_t)y * S + x0;
-  const float mean[3] = {m0, m1, m2}, sd[3] = {s0_, s1_, s2_};
+  float v[3][4];
 #pragma unroll
   for (int px = 0; px < 4; ++px)
-    if (x0 + px < S)
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        out[o + c * plane + px] = ((float)clip8(acc[3 * px + c]) / 255.0f - mean[c]) / sd[c];
+    for (int c = 0; c < 3; ++c) v[c][px] = lut[c][clip8(acc[3 * px + c])];
+  if ((S & 3) == 0) {  // 16-byte aligned quads: one dwordx4 store per plane
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      *(float4*)(out + o + c * plane) = make_float4(v[c][0], v[c][1], v[c][2], v[c][3]);
+  } else {
+#pragma unroll
+    for (int px = 0; px < 4; ++px)
+      if (x0 + px < S)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) out[o + c * plane + px] = v[c][px];
+  }
 }
 
 __global__ __launch_bounds__(NT) void nearest_mask_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
@@ -378,9 +462,30 @@ int tmp_stride(int S) { return (S * 3 + 12 + 15) & ~15; }  // + 12: the last 4-p
 constexpr int H_LDS = 64 * 1024;
 // bytes of LDS the horizontal pass needs for `rows` source rows (0 = does not fit)
 int h_lds_bytes(int in_w, int rows, int* srow) {
-  *srow = (in_w * 3 + 3 + 3 + 3 * HK + 8 + 15) & ~15;  // + 3*HK + 8: zero-weight taps / dword tail
+  *srow = (in_w * 3 + 15 + 15 + 3 * HK + 8 + 15) & ~15;  // + 3*HK + 8: zero-weight taps / read tail
   const int64_t bytes = (int64_t)rows * *srow;
   return bytes <= H_LDS ? (int)bytes : 0;
+}
+
+// register tap slots for one axis: an upper bound on every output coordinate's tap
+// count (xmax - xmin <= floor(2 * support) + 1; + 1 more against rounding in the
+// plan's double arithmetic), at most the plan's ksize, rounded up to even; 0 when it
+// exceeds HK (the fixed-slot kernels do not apply). Slots past a coordinate's count
+// carry weight 0 in the plan, so fewer slots than ksize lose nothing.
+int tap_slots(int in_size, int out_size, int ksize) {
+  const double scale = (double)in_size / out_size;
+  const double support = 2.0 * (scale < 1.0 ? 1.0 : scale);
+  const int n = std::min(ksize, (int)floor(2.0 * support) + 2);
+  const int k = std::max(4, (n + 1) & ~1);
+  return k <= HK ? k : 0;
+}
+
+template <int K>
+int launch_h(const HArgs& h, dim3 grid, int block, int lds, hipStream_t st) {
+  static unsigned done = 0;
+  if (!lds_attr_once((const void*)resample_h_kernel<K>, H_LDS, done)) return AACLIP_ERR_LAUNCH;
+  resample_h_kernel<K><<<grid, block, lds, st>>>(h);
+  return AACLIP_OK;
 }
 }  // namespace
 
@@ -426,30 +531,45 @@ extern "C" int aaclip_preprocess_images(const uint8_t* src, int64_t img_stride, 
   if (const char* e = getenv("AACLIP_PREP_HROWS")) hrows = std::max(1, atoi(e));  // tuning
   while (hrows > 0 && !(hlds = h_lds_bytes(in_w, hrows, &srow))) hrows >>= 1;
   const int tstride = tmp_stride(out_size);
-  if (workspace && workspace_bytes >= (size_t)batch * in_h * tstride && hlds && kx <= HK && out_size <= 1024 &&
-      batch <= 65535 &&
+  if (workspace && workspace_bytes >= (size_t)batch * in_h * tstride && hlds && tap_slots(in_w, out_size, kx) &&
+      out_size <= 1024 && batch <= 65535 &&
       !getenv("AACLIP_PREP_TILE")) {
-    static unsigned h8_dev = 0, hk_dev = 0;
-    if (!lds_attr_once((const void*)resample_h_kernel<8>, H_LDS, h8_dev) ||
-        !lds_attr_once((const void*)resample_h_kernel<HK>, H_LDS, hk_dev))
-      return AACLIP_ERR_LAUNCH;
     HArgs h{src, img_stride, row_pitch, in_h, in_w, out_size, hrows, x_bounds, x_coeffs, kx, srow, tstride,
             (uint8_t*)workspace};
     const dim3 hgrid(ceil_div(in_h, hrows), batch);
-    if (kx <= 8)
-      resample_h_kernel<8><<<hgrid, 64 * ceil_div(out_size, 64), hlds, (hipStream_t)stream>>>(h);
-    else
-      resample_h_kernel<HK><<<hgrid, 64 * ceil_div(out_size, 64), hlds, (hipStream_t)stream>>>(h);
+    const hipStream_t st = (hipStream_t)stream;
+    int rc = AACLIP_ERR_ARG;
+    switch (tap_slots(in_w, out_size, kx)) {
+#define AACLIP_H_CASE(K) \
+  case K:                \
+    rc = launch_h<K>(h, hgrid, 64 * ceil_div(out_size, 64), hlds, st); \
+    break;
+      AACLIP_H_CASE(4) AACLIP_H_CASE(6) AACLIP_H_CASE(8) AACLIP_H_CASE(10) AACLIP_H_CASE(12) AACLIP_H_CASE(14)
+      AACLIP_H_CASE(16)
+#undef AACLIP_H_CASE
+    }
+    if (rc != AACLIP_OK) return rc;
     AACLIP_CHECK_LAUNCH();
-    resample_v_kernel<<<dim3(ceil_div(out_size, 256), out_size, batch), 64, 0, (hipStream_t)stream>>>(
-        (const uint8_t*)workspace, in_h, out_size, tstride, y_bounds, y_coeffs, ky, a.mean[0], a.mean[1],
-        a.mean[2], a.stdv[0], a.stdv[1], a.stdv[2], out);
+    const dim3 vgrid(ceil_div(out_size * ceil_div(out_size, 4), 256), batch);
+    const VArgs v{(const uint8_t*)workspace, in_h, out_size, tstride, y_bounds, y_coeffs, ky,
+                  {a.mean[0], a.mean[1], a.mean[2]}, {a.stdv[0], a.stdv[1], a.stdv[2]}, out};
+    switch (tap_slots(in_h, out_size, ky)) {
+#define AACLIP_V_CASE(K) \
+  case K:                \
+    resample_v_kernel<K><<<vgrid, 256, 0, st>>>(v); \
+    break;
+      AACLIP_V_CASE(4) AACLIP_V_CASE(6) AACLIP_V_CASE(8) AACLIP_V_CASE(10) AACLIP_V_CASE(12) AACLIP_V_CASE(14)
+      AACLIP_V_CASE(16)
+#undef AACLIP_V_CASE
+      default:
+        resample_v_kernel<0><<<vgrid, 256, 0, st>>>(v);
+    }
     AACLIP_CHECK_LAUNCH();
     return AACLIP_OK;
   }
   // single-kernel path (no workspace, or rows too wide for LDS): tile choice: the tallest/widest staged tile (from 16 x 32) whose weights + strip + patch
   // fit STAGED_LDS, else direct taps. 1024 -> 336: 16 x 32 tiles, 62 x 111-pixel patches,
-  // 32 KB -> 4 workgroups per CU. Measured at B=32 1024^2 (tools/prep_sweep.sh):
+  // 32 KB -> 4 workgroups per CU. Measured at B=32 1024^2 (AACLIP_PREP_TILE + kbench --only prep):
   // 16x64 257 us, 8x64 195, 16x32 152, 16x16 144, direct 257 -- occupancy-bound.
   bool staged = false;
   int lds = 0;
