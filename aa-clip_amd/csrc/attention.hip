@@ -46,6 +46,27 @@ __device__ __forceinline__ float max_over_groups(float v) {
   return m;
 }
 
+// Max of a lane's 4 x NKB scores as a tree of v_max3 (depth 3 for 16 values instead
+// of a 16-long dependent chain; max is exact, so the order does not change the bits).
+template <int NKB>
+__device__ __forceinline__ float tile_lane_max(const float4_t (&st)[NKB]) {
+  if constexpr (NKB == 4) {
+    const float a = fmaxf(fmaxf(st[0][0], st[0][1]), st[0][2]);
+    const float b = fmaxf(fmaxf(st[0][3], st[1][0]), st[1][1]);
+    const float c = fmaxf(fmaxf(st[1][2], st[1][3]), st[2][0]);
+    const float d = fmaxf(fmaxf(st[2][1], st[2][2]), st[2][3]);
+    const float e = fmaxf(fmaxf(st[3][0], st[3][1]), st[3][2]);
+    return fmaxf(fmaxf(fmaxf(a, b), c), fmaxf(fmaxf(d, e), st[3][3]));
+  } else {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[kb][i]);
+    return mx;
+  }
+}
+
 // One 64-key tile for one wave: NKB live 16-key blocks (1, 2 or 4), NQB live
 // 16-query blocks (1 or 2), MASK = tile needs the key-tail / causal mask.
 // Dead blocks and the mask are resolved at compile time, so the 577 = 9*64 + 1
@@ -107,15 +128,16 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const h16x8_t<H16>
           mx = fmaxf(mx, sv);
         }
     } else {
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[qb][kb][i]);
+      mx = tile_lane_max<NKB>(st[qb]);
     }
-    mx = max_over_groups(mx);  // max over the tile of S' - m for this lane's query
-    const bool move = first || mx > kRescaleLog2;
-    if (__builtin_amdgcn_ballot_w64(move) != 0) {  // wave-uniform branch, rare after the first tile
-      const float d = move ? mx : 0.f;          // tile 0 always has a valid key: mx is finite
+    // The deferred max only moves when some query's tile max beats it by 2^8. A query's
+    // max is the max of its 4 lanes' maxes, so "no lane's own max exceeds the bound"
+    // (one ballot) means no query moves: the cross-lane reduction runs only on the
+    // rare rescale path (and on tile 0).
+    if (__builtin_amdgcn_ballot_w64(first || mx > kRescaleLog2) != 0) {  // wave-uniform, rare after tile 0
+      mx = max_over_groups(mx);  // max over the tile of S' - m for this lane's query
+      const bool move = first || mx > kRescaleLog2;
+      const float d = move ? mx : 0.f;  // tile 0 always has a valid key: mx is finite
       m_run[qb] += d;
       const float alpha = __builtin_amdgcn_exp2f(-d);
       l_acc[qb][0] *= alpha;  // only element 0 is read at the end
@@ -194,14 +216,10 @@ __device__ __forceinline__ void attn_tile_split(const char* kt_lds, const h16x8_
       }
   };
   auto max_decide = [&](int qb, float4_t (&st)[4]) {
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[kb][i]);
-    mx = max_over_groups(mx);
-    const bool move = first || mx > kRescaleLog2;
-    if (__builtin_amdgcn_ballot_w64(move) != 0) {
+    float mx = tile_lane_max<4>(st);
+    if (__builtin_amdgcn_ballot_w64(first || mx > kRescaleLog2) != 0) {  // lane-local check, as attn_tile
+      mx = max_over_groups(mx);
+      const bool move = first || mx > kRescaleLog2;
       const float d = move ? mx : 0.f;
       m_run[qb] += d;
       const float alpha = __builtin_amdgcn_exp2f(-d);
