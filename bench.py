@@ -465,9 +465,17 @@ def main():
     if args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU "
                  "(plain `python bench.py --gpus N` starts them itself)")
+    # AACLIP_BENCH_REHEARSAL=1: every rank on cuda:0 over gloo -- exercises the N-rank launch,
+    # sharding, all-gather and max-over-ranks timing on a one-GPU box (not a scaling number)
+    rehearsal = os.environ.get("AACLIP_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -532,7 +540,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (N(0,1) images on device, random-init ViT-L/14-336 + adapters)",
+        "data": "synthetic (N(0,1) images on device, random-init ViT-L/14-336 + adapters)"
+                + (" [REHEARSAL: all ranks on cuda:0 over gloo]" if rehearsal else ""),
         "config": {"workload": f"C2: AA-CLIP anomaly-map inference, ViT-L/14-336, {args.dtype}, 4 levels, 2 anchors, "
                                "Industrial blur, per-GPU batch of images",
                    "global_batch": n_total, "img_size": S, "per_gpu_batch": B,
