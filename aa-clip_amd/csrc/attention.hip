@@ -566,69 +566,159 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
 }
 
 // ---------------------------------------------------------------- fp32 (parity mode)
-// One thread per query; 64 queries per block; K/V tiles of 64 keys in LDS
-// (every lane reads the same K/V row -> LDS broadcast).
-__global__ __launch_bounds__(64) void attn_f32_kernel(const float* __restrict__ qkv,
-                                                      float* __restrict__ out, int N, int H,
-                                                      int causal) {
-  __shared__ float Ks[KT][HD_];
-  __shared__ float Vs[KT][HD_];
+// Flash attention on v_mfma_f32_16x16x4f32 (exact fp32 products, fp32 accumulation; the
+// fp32 matrix rate is the fp32 vector peak, and the softmax VALU is small beside it).
+// Workgroup = 4 waves x 32 queries of one (image, head); K/V tiles of 64 keys staged
+// through registers into row-padded LDS (68 floats per row: the strided fragment reads
+// below are bank-conflict-free); the next tile's global loads are in flight while the
+// current one is computed. Same swapped layout as the 16-bit kernel: S^T = K . Q^T puts
+// one query's scores on the 4 lanes {fr, fr+16, fr+32, fr+48}, and each lane's own P
+// registers are the B operand of O^T = V^T . P^T (the key order inside a 4-key MFMA step
+// is the lane group's). Online softmax in the log2 domain (log2(e)/8 folded into Q).
+constexpr int F32_LDK = 68;
+
+__global__ __launch_bounds__(256, 2) void attn_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                          int N, int H, int causal) {
+  constexpr int QB = 2;  // 16-query blocks per wave
+  __shared__ __attribute__((aligned(16))) float Ks[KT][F32_LDK];
+  __shared__ __attribute__((aligned(16))) float Vs[KT][F32_LDK];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh % H;
   const int HDt = H * HD_;
   const int64_t ld = 3 * (int64_t)HDt;
   const float* base = qkv + (size_t)b * N * ld + h * HD_;
-  const int q = blockIdx.x * 64 + threadIdx.x;
-  const int qc = min(q, N - 1);
-  float qv[HD_], o[HD_];
+  const int q0 = blockIdx.x * 128 + wid * 32;
+  const bool active = q0 < N;
+
+  constexpr float qscale = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+  float qv[QB][16];  // Q[q][4s + fq] for this lane's query q = q0 + 16 qb + fr
 #pragma unroll
-  for (int d = 0; d < HD_; ++d) {
-    qv[d] = base[(size_t)qc * ld + d] * 0.125f;
-    o[d] = 0.f;
+  for (int qb = 0; qb < QB; ++qb) {
+    const float* qr = base + (size_t)min(q0 + qb * 16 + fr, N - 1) * ld;
+#pragma unroll
+    for (int s4 = 0; s4 < 16; ++s4) qv[qb][s4] = qr[4 * s4 + fq] * qscale;
   }
-  float m = -INFINITY, l = 0.f;
+
   int ntiles = (N + KT - 1) / KT;
-  if (causal) ntiles = min(ntiles, min(blockIdx.x * 64 + 63, N - 1) / KT + 1);
-  for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < KT * HD_; i += 64) {
-      const int r = i / HD_, d = i % HD_;
-      const int key = min(t * KT + r, N - 1);
-      Ks[r][d] = base[(size_t)key * ld + HDt + d];
-      Vs[r][d] = base[(size_t)key * ld + 2 * HDt + d];
-    }
-    __syncthreads();
-    float s[KT];
-    float mx = -INFINITY;
-#pragma unroll 4
-    for (int j = 0; j < KT; ++j) {
-      float acc = 0.f;
+  if (causal) ntiles = min(ntiles, min((int)blockIdx.x * 128 + 127, N - 1) / KT + 1);
+
+  // staging: thread t moves float4 number t + 256 j (j < 4) of the K and of the V tile
+  float4_t kreg[4], vreg[4];
+  auto load_tile = [&](int tile) {
 #pragma unroll
-      for (int d = 0; d < HD_; ++d) acc = fmaf(qv[d], Ks[j][d], acc);
-      const int key = t * KT + j;
-      if (key >= N || (causal && key > qc)) acc = -INFINITY;
-      s[j] = acc;
-      mx = fmaxf(mx, acc);
+    for (int j = 0; j < 4; ++j) {
+      const int f = t + 256 * j, r = f >> 4, c4 = f & 15;
+      const float* src = base + (size_t)min(tile * KT + r, N - 1) * ld + HDt + 4 * c4;
+      kreg[j] = *(const float4_t*)src;
+      vreg[j] = *(const float4_t*)(src + HDt);
     }
-    const float m_new = fmaxf(m, mx);
-    const float alpha = expf(m - m_new);
-    l *= alpha;
+  };
+  auto store_tile = [&]() {
 #pragma unroll
-    for (int d = 0; d < HD_; ++d) o[d] *= alpha;
-#pragma unroll 4
-    for (int j = 0; j < KT; ++j) {
-      const float p = expf(s[j] - m_new);
-      l += p;
-#pragma unroll
-      for (int d = 0; d < HD_; ++d) o[d] = fmaf(p, Vs[j][d], o[d]);
+    for (int j = 0; j < 4; ++j) {
+      const int f = t + 256 * j, r = f >> 4, c4 = f & 15;
+      *(float4_t*)&Ks[r][4 * c4] = kreg[j];
+      *(float4_t*)&Vs[r][4 * c4] = vreg[j];
     }
-    m = m_new;
+  };
+
+  float4_t o[QB][4];
+  float m[QB], l[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+#pragma unroll
+    for (int db = 0; db < 4; ++db) o[qb][db] = float4_t{0.f, 0.f, 0.f, 0.f};
+    m[qb] = -INFINITY;
+    l[qb] = 0.f;
   }
-  if (q < N) {
-    float* op = out + ((size_t)b * N + q) * HDt + h * HD_;
-    const float inv = 1.0f / l;
+
+  load_tile(0);
+  store_tile();
+  __syncthreads();
+  for (int tile = 0; tile < ntiles; ++tile) {
+    if (tile + 1 < ntiles) load_tile(tile + 1);  // lands while this tile is computed
+    if (active) {
+      const int key0 = tile * KT;
+      float4_t st[QB][4];
 #pragma unroll
-    for (int d = 0; d < HD_; ++d) op[d] = o[d] * inv;
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) st[qb][kb] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+          const float kf = Ks[kb * 16 + fr][4 * s4 + fq];
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb)
+            st[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf, qv[qb][s4], st[qb][kb], 0, 0, 0);
+        }
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        // st[qb][kb][e] = score of key key0 + 16 kb + 4 fq + e for query q
+        const int q = q0 + qb * 16 + fr;
+        const int lim = (causal ? min(N, q + 1) : N) - key0 - 4 * fq;  // valid: 16 kb + e < lim
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = (16 * kb + e < lim) ? st[qb][kb][e] : -INFINITY;
+            st[qb][kb][e] = v;
+            mx = fmaxf(mx, v);
+          }
+        mx = max_over_groups(mx);
+        const float mn = fmaxf(m[qb], mx);
+        const float mu = mn == -INFINITY ? 0.f : mn;  // no valid key yet: keep p = 0, alpha = 1
+        const float alpha = __builtin_amdgcn_exp2f(m[qb] - mu);
+        m[qb] = mn;
+        float ls = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float p = __builtin_amdgcn_exp2f(st[qb][kb][e] - mu);
+            st[qb][kb][e] = p;
+            ls += p;
+          }
+        l[qb] = l[qb] * alpha + ls;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) o[qb][db] *= alpha;
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float vf = Vs[kb * 16 + 4 * fq + i][db * 16 + fr];
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+              o[qb][db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, st[qb][kb][i], o[qb][db], 0, 0, 0);
+          }
+    }
+    __syncthreads();
+    if (tile + 1 < ntiles) {
+      store_tile();
+      __syncthreads();
+    }
+  }
+  if (!active) return;
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    // the query's row sum is split over its 4 lane groups
+    auto a2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l[qb]), __float_as_uint(l[qb]), false, false);
+    float lt = __uint_as_float(a2[0]) + __uint_as_float(a2[1]);
+    auto b2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+    lt = __uint_as_float(b2[0]) + __uint_as_float(b2[1]);
+    const int q = q0 + qb * 16 + fr;
+    if (q < N) {
+      float* op = out + ((size_t)b * N + q) * HDt + h * HD_ + 4 * fq;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) *(float4_t*)(op + 16 * db) = o[qb][db] / lt;
+    }
   }
 }
 
@@ -680,8 +770,8 @@ extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch
       else launch_attn<false, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
     }
   } else {
-    dim3 grid(ceil_div(seq, 64), batch * heads);
-    attn_f32_kernel<<<grid, 64, 0, s>>>((const float*)qkv, (float*)out, seq, heads, flags & AACLIP_ATTN_CAUSAL);
+    dim3 grid(ceil_div(seq, 128), batch * heads);
+    attn_f32_kernel<<<grid, 256, 0, s>>>((const float*)qkv, (float*)out, seq, heads, flags & AACLIP_ATTN_CAUSAL);
   }
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
