@@ -10,7 +10,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "aa-clip_amd")]
 from aaclip import _lib, ops  # noqa: E402
-from tools.splitk_ab import graph_time  # noqa: E402
+from tools.map_bench import graph_time  # noqa: E402
 
 
 def main():
