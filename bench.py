@@ -181,6 +181,42 @@ def preprocess_leg(dev, batch, size, reps=20):
                          "algorithmic_bytes_per_launch": alg, "traffic": None}}
 
 
+def metrics_leg(dev, size, reps=5):
+    """SURVEY 8(f)-1 on device: one class's metrics_eval (class min-max, pixel-max score
+    fusion, exact tie-aware pixel/image AUROC + AP: rocPRIM radix sort of 33-bit keys,
+    scans, fixed-order reductions), graph-timed, at a C4 batch (32 images) and at the
+    largest MVTec test class (167 images). Synthetic maps (uniform scores) and masks
+    (5 % anomalous pixels). Sort-bound, not a streaming kernel: the exact tie-aware
+    metrics need the class's pixels in score order (one radix sort of 64-bit keys), so
+    the figure is pixels ranked per second, with the per-class time beside the class's
+    forward (32 images: ~14 ms)."""
+    import ctypes
+    from aaclip import _lib
+    out = {}
+    for n_img in (32, 167):
+        pix = size * size
+        g = torch.Generator(device=dev).manual_seed(9)
+        preds = torch.rand(n_img, pix, device=dev, generator=g)
+        lab = (torch.rand(n_img, pix, device=dev, generator=g) < 0.05).to(torch.uint8)
+        ip = torch.rand(n_img, device=dev, generator=g)
+        il = (torch.arange(n_img, device=dev) % 2).to(torch.uint8)
+        need = ctypes.c_size_t(0)
+        _lib.call("aaclip_metrics_workspace", n_img * pix, n_img, ctypes.byref(need))
+        wsb = torch.empty(int(need.value) + 256, device=dev, dtype=torch.uint8)
+        off = (-wsb.data_ptr()) % 256
+        res = torch.empty(4, device=dev, dtype=torch.float64)
+
+        def run():
+            _lib.call("aaclip_metrics_eval", preds.data_ptr(), lab.data_ptr(), ip.data_ptr(), il.data_ptr(), n_img,
+                      pix, 0, wsb.data_ptr() + off, need.value, res.data_ptr(),
+                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        t = time_launches(run, reps, torch.cuda.current_stream())
+        out[f"class_{n_img}_images"] = {"pixels": n_img * pix, "ms": round(t, 3),
+                                        "mpixels_per_sec": round(n_img * pix / (t * 1e-3) / 1e6, 1)}
+    out["bound"] = "sort (rocPRIM radix sort of 64-bit keys + scans), exact sklearn-equivalent AUROC/AP"
+    return out
+
+
 def roofline_gemm(eng, ws, reps=20):
     """Dominant kernel = the bf16 MFMA GEMM (QKV and c_fc launches; which tile family
     the per-shape dispatch picks is reported). Average HIP-event launch duration over
@@ -563,6 +599,7 @@ def main():
         line["cpu_baseline"], line["parity"] = cpu_baseline_and_parity(dev, n_streams, args.cpu_seconds)
     if rank == 0 and world == 1 and not args.no_roofline:
         line["preprocess"] = preprocess_leg(dev, B, S)
+        line["metrics"] = metrics_leg(dev, S)
     if rank == 0 and world == 1 and not args.no_c5:
         del eng, run, vp, ad
         torch.cuda.empty_cache()
