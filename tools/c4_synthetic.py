@@ -123,6 +123,7 @@ def main():
             maps = R.anomaly_map(seg, Tc, 336, DOMAINS[DS])
             sc = R.image_score(det, Tc)
             ref[c] = (Tc, R.metrics_eval(msk[:, 0], lab, maps, sc, c, DOMAINS[DS]), maps, sc)
+            print(f"cpu reference: class {c} done ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
         cpu_dt = time.perf_counter() - t0
         for tag, dt_ in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
             model = build(dev, dt_)
