@@ -10,7 +10,7 @@ import ctypes
 import os
 
 LIB_PATH = os.environ.get("AACLIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaaclip_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 F32 = 0
 BF16 = 1
@@ -40,6 +40,7 @@ SIGNATURES = {
     "aaclip_quant_fp8_mx": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _P],
     "aaclip_set_gemm_variant": [_I],
     "aaclip_gemm_pin": [_I, _I, _I, _I, _I],
+    "aaclip_gemm_concurrent": [_I, ctypes.POINTER(_I)],
     "aaclip_gemm_plan": [_I, _I, _I, _I],
     "aaclip_attention": [_I, _P, _P, _I, _I, _I, _I, _I, _P, _L, _P],
     "aaclip_set_attn_variant": [_I],

@@ -348,33 +348,6 @@ class VisualEngine:
         P = out[0].shape[0] // B
         return [y.view(B, P, EMBED) for y in out], det
 
-    def _concurrent_pins(self, sizes, S):
-        """Chunks on concurrent streams share the CUs, so one chunk's partial last
-        round of GEMM tiles is filled by the other's work, and the 8-phase 256x256
-        tile (faster per FLOP) wins even where its tile count rounds up worse than
-        the 320-row tile's: c_fc at 16 images per chunk, whole two-stream C2 step
-        2240 -> 2290 images/s bf16 (2164 -> 2220 fp16); a single stream keeps the
-        heuristic (1895 vs 2050). Pins the 8-phase family for the chunks' block-GEMM
-        shapes that fill at least one round with it; returns what to restore (the
-        dispatch happens at launch, so the pins only need to hold while the chunks
-        are enqueued, graph capture included)."""
-        if self.dtype not in (torch.bfloat16, torch.float16):
-            return []
-        tag = ops.dtag(torch.empty(0, dtype=self.dtype))
-        cus = torch.cuda.get_device_properties(self.device).multi_processor_count
-        n_tok = (S // PATCH) ** 2 + 1
-        shapes = ((3 * WIDTH, WIDTH), (WIDTH, WIDTH), (4 * WIDTH, WIDTH), (WIDTH, 4 * WIDTH))
-        pinned = []
-        for b in sorted(set(sizes)):
-            M = b * n_tok
-            for N, K in shapes:
-                key = (tag, M, N, K)
-                if key in ops._tuned or -(-M // 256) * (N // 256) < cus or M * K * 2 >= 1 << 31:
-                    continue
-                ops.pin_gemm(tag, M, N, K, 3)
-                pinned.append(key)
-        return pinned
-
     def _chunk_streams(self, n: int):
         if len(getattr(self, "_streams", [])) < n:
             self._streams = [torch.cuda.Stream(device=self.device) for _ in range(n)]
@@ -433,8 +406,17 @@ class VisualEngine:
         sts = self._chunk_streams(nstreams)
         for st in sts:
             st.wait_event(ready)
-        pinned = self._concurrent_pins(sizes, S) if nstreams > 1 else []
-        try:
+        # every chunk's workspace exists (and, with AACLIP_GEMM_TUNE, is tuned) before any
+        # chunk is enqueued: tuning never runs beside the other streams' kernels
+        for i in range(len(sizes)):
+            self._workspace(sizes[i], S, _slot0 + i % nstreams)
+        # concurrent chunks share the CUs: one chunk's partial last round of GEMM tiles is
+        # filled by the other's work, so the 8-phase 256x256 tile (faster per FLOP) wins
+        # even where its tile count rounds up worse than the 320-row tile's (c_fc at 16
+        # images per chunk): whole two-stream C2 step 2240 -> 2295 images/s bf16 (2164 ->
+        # 2220 fp16); a single stream keeps the heuristic (1895 vs 2050). Thread-local
+        # (aaclip_gemm_concurrent), chosen at launch, so graph capture keeps it.
+        with ops.concurrent_gemms(nstreams > 1 and self.dtype in (torch.bfloat16, torch.float16)):
             for i in range(len(sizes)):
                 b0, b1 = bounds[i], bounds[i + 1]
                 st = sts[i % nstreams]
@@ -443,9 +425,6 @@ class VisualEngine:
                     ops.anomaly_map(seg_raw, T, out_map[b0:b1], ws["grid"], g=ws["g"], ksize=k, sigma=s)
                     ops.image_score(det_raw, b1 - b0, ws["P"], ws["partial"], det=ws["det"], T=T,
                                     score=out_score[b0:b1])
-        finally:
-            for key in pinned:
-                ops.pin_gemm(*key, 0)
         for st, ev in zip(sts, done):
             ev.record(st)
             main.wait_event(ev)

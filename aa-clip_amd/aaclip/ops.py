@@ -97,6 +97,29 @@ def pin_gemm(dtype: int, M: int, N: int, K: int, family: int) -> None:
     call("aaclip_gemm_pin", dtype, M, N, K, family)
 
 
+class concurrent_gemms:
+    """Context manager: aaclip_gemm_concurrent for the calling thread while image chunks
+    are enqueued on concurrent streams (block-GEMM shapes that fill a round of the CUs
+    take the 8-phase kernel; bit-identical). Restores the previous state on exit."""
+
+    def __init__(self, on: bool = True):
+        self.on = int(bool(on))
+        self.prev = ctypes.c_int(0)
+
+    def __enter__(self):
+        call("aaclip_gemm_concurrent", self.on, ctypes.byref(self.prev))
+        return self
+
+    def __exit__(self, *exc):
+        call("aaclip_gemm_concurrent", self.prev.value, None)
+        return False
+
+
+def gemm_plan(tag: int, M: int, N: int, K: int) -> str:
+    """Kernel name aaclip_gemm launches for this shape on this thread (reports)."""
+    return _lib.lib().aaclip_gemm_plan(tag, M, N, K).decode()
+
+
 def tune_gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, reps: int = 3, **epilogue) -> int:
     """Measure every tile family on these operands with this epilogue (HIP events on the
     current stream) and pin the fastest for the shape (aaclip_gemm_pin). The families

@@ -21,6 +21,9 @@
 //   64x64x16 register-staged tiles. Same epilogue.
 #include <math.h>
 
+#include <atomic>
+#include <mutex>
+
 #include "common.h"
 
 namespace {
@@ -1006,19 +1009,72 @@ int g_group_m = 8;
 int g_setprio = 0;
 int g_dbg = 0;
 
-// Per-shape pinned tile family (aaclip_gemm_pin): measured choice for a (dtype, M, N, K)
-// that overrides the heuristic. Written at engine setup (host), read by every launch.
+// Per-shape pinned tile family (aaclip_gemm_pin): a measured choice for one
+// (dtype, M, N, K) that overrides the heuristic. Written by a tuner (host), read by
+// every launch; guarded by a mutex (two engines may launch from two threads --
+// ctypes releases the GIL). Unpinning removes the entry, so the table holds only
+// live pins and cannot fill up with dead ones.
 struct Pin {
   int dtype, M, N, K, fam;
 };
 constexpr int kPins = 256;
 Pin g_pins[kPins];
-int g_npins = 0;
+std::atomic<int> g_npins{0};
+std::mutex g_pin_mu;
 
 int pinned_family(int dtype, int M, int N, int K) {
-  for (int i = 0; i < g_npins; ++i)
+  if (g_npins.load(std::memory_order_acquire) == 0) return 0;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  const int n = g_npins.load(std::memory_order_relaxed);
+  for (int i = 0; i < n; ++i)
     if (g_pins[i].dtype == dtype && g_pins[i].M == M && g_pins[i].N == N && g_pins[i].K == K) return g_pins[i].fam;
   return 0;
+}
+
+// Concurrent-chunk mode (aaclip_gemm_concurrent), per HOST THREAD: while a thread
+// enqueues image chunks on concurrent streams, every block-GEMM shape whose 256x256
+// tiles fill at least one round of the CUs takes the 8-phase kernel. The other
+// chunk's work fills the partial last round, and the 8-phase tile is faster per
+// FLOP (two-stream C2 step 2240 -> 2295 images/s bf16). The choice is made at
+// launch (captured graphs keep it); thread-local, so it needs no global pin state.
+thread_local int t_concurrent = 0;
+
+enum Kern { KERN_256x256 = 1, KERN_256x128 = 2, KERN_8PH = 3, KERN_8PH_PERSIST = 5, KERN_320x256 = 8,
+            KERN_128x128 = 9 };
+
+// The kernel a 16-bit GEMM of this shape launches: the A/B variant hook, else a pin,
+// else the concurrent-chunk rule, else the per-shape heuristic (fewer tile rounds
+// over the CUs, weighted by per-tile cost). M = B*577 tiles unevenly: 320-row tiles
+// of the LDS-DMA kernel vs 256-row tiles of the 8-phase kernel (~10 % faster per
+// FLOP). E.g. at 16 images per stream (M = 9232) the 8-phase kernel wins on QKV,
+// out-proj, c_proj and adapters (148-444 tiles) and the 320-row one on c_fc (464 vs
+// 592 tiles = 2 vs 3 rounds); measured per shape with tools/kbench.py.
+int choose16(int dtype, int M, int N, int K, bool fits) {
+  int fam = g_gemm_variant ? g_gemm_variant : pinned_family(dtype, M, N, K);
+  if (!fam && t_concurrent && N % 256 == 0 && fits && (int64_t)ceil_div(M, 256) * (N / 256) >= cu_count())
+    fam = KERN_8PH;
+  switch (fam) {
+    case 1: return KERN_256x256;
+    case 2: return KERN_256x128;
+    case 3:
+    case 4:  // 8-phase for the wide GEMMs only (N >= 2048), 320x256 below
+      if (N % 256 == 0 && (fam == 3 || N >= 2048) && fits) return KERN_8PH;
+      break;
+    case 5:  // A/B: the persistent 8-phase kernel wherever N % 256 == 0
+      if (N % 256 == 0 && fits) return KERN_8PH_PERSIST;
+      break;
+    case 9: return KERN_128x128;  // 128x128 everywhere (A/B)
+    case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
+      if (N % 256 == 0) return KERN_320x256;
+      break;
+    default: break;
+  }
+  if (N % 256 == 0 && fam == 0) {
+    const bool ph8 = fits && prefer_8ph(M, N);
+    if (prefer_small(M, N, ph8)) return KERN_128x128;
+    if (ph8) return KERN_8PH;
+  }
+  return N % 256 == 0 ? KERN_320x256 : KERN_256x128;
 }
 
 // 16-bit dispatch (bf16 or fp16 operands; same tiles, same per-shape choice)
@@ -1027,82 +1083,61 @@ int dispatch16(GemmArgs a, hipStream_t s) {
   const int M = a.M, N = a.N;
   if (a.K % 64 || N % 128) return AACLIP_ERR_ARG;
   const bool fits = (int64_t)M * a.lda * 2 < (1ll << 31) && (int64_t)N * a.ldw * 2 < (1ll << 31);
-  const int fam = g_gemm_variant ? g_gemm_variant : pinned_family(H16 ? AACLIP_F16 : AACLIP_BF16, M, N, a.K);
-  switch (fam) {
-    case 1: return launch_bf16<256, 256, 2, 4, 0, H16>(a, s);
-    case 2: return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
-    case 3:
-    case 4:  // 8-phase for the wide GEMMs only (N >= 2048), 320x256 below
-      if (N % 256 == 0 && (fam == 3 || N >= 2048) && fits) return launch_bf16_8ph<H16>(a, s);
-      break;
-    case 5:  // A/B: the persistent 8-phase kernel wherever N % 256 == 0
-      if (N % 256 == 0 && fits) return launch_bf16_8ph<H16, true>(a, s);
-      break;
-    case 9: return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);  // 128x128 everywhere (A/B)
-    case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
-      if (N % 256 == 0) return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
-      break;
-    default: break;
+  switch (choose16(H16 ? AACLIP_F16 : AACLIP_BF16, M, N, a.K, fits)) {
+    case KERN_256x256: return launch_bf16<256, 256, 2, 4, 0, H16>(a, s);
+    case KERN_8PH: return launch_bf16_8ph<H16>(a, s);
+    case KERN_8PH_PERSIST: return launch_bf16_8ph<H16, true>(a, s);
+    case KERN_320x256: return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
+    case KERN_128x128: return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);
+    default: return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
   }
-  // Default: per shape, the kernel with the fewer tile rounds weighted by its per-tile
-  // cost. M = B*577 tiles unevenly: 320-row tiles of the LDS-DMA kernel vs 256-row
-  // tiles of the 8-phase kernel (~10 % faster per FLOP). E.g. in the two-stream
-  // pipeline (16 images per stream, M = 9232) the 8-phase kernel wins on QKV, out-proj,
-  // c_proj and adapters (148-444 tiles) and the 320-row one on c_fc (464 vs 592 tiles
-  // = 2 vs 3 rounds); measured per shape with tools/kbench.py, whole C2 step +5 %.
-  if (N % 256 == 0 && fam == 0) {
-    const bool ph8 = fits && prefer_8ph(M, N);
-    if (prefer_small(M, N, ph8)) return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);
-    if (ph8) return launch_bf16_8ph<H16>(a, s);
-  }
-  if (N % 256 == 0) return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
-  return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
 }
 
 }  // namespace
 
-// Which kernel aaclip_gemm launches for this shape (same decision as the dispatch
-// below; for reports such as bench.py's roofline label). Host only.
+// Which kernel aaclip_gemm launches for this shape (same decision as the dispatch,
+// for operands with lda = ldw = K, on the calling thread). Host only, for reports.
 extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
   if (in_dtype != AACLIP_BF16 && in_dtype != AACLIP_F16) return "gemm_f32_kernel";
   if (M <= 0 || N % 128 || K % 64) return "invalid";
-  const int fam = g_gemm_variant ? g_gemm_variant : pinned_family(in_dtype, M, N, K);
-  switch (fam) {
-    case 1: return "gemm_bf16_kernel<256,256,2,4>";
-    case 2: return "gemm_bf16_kernel<256,128,4,2>";
-    case 3:
-    case 4:
-      if (N % 256 == 0 && (fam == 3 || N >= 2048)) return "gemm_bf16_8ph_kernel<256,256>";
-      break;
-    case 5:
-      if (N % 256 == 0) return "gemm_bf16_8ph_kernel<256,256,persistent>";
-      break;
-    case 8:
-      if (N % 256 == 0) return "gemm_bf16_kernel<320,256,2,4>";
-      break;
-    default: break;
+  const bool fits = (int64_t)M * K * 2 < (1ll << 31) && (int64_t)N * K * 2 < (1ll << 31);
+  switch (choose16(in_dtype, M, N, K, fits)) {
+    case KERN_256x256: return "gemm_bf16_kernel<256,256,2,4>";
+    case KERN_8PH: return "gemm_bf16_8ph_kernel<256,256>";
+    case KERN_8PH_PERSIST: return "gemm_bf16_8ph_kernel<256,256,persistent>";
+    case KERN_320x256: return "gemm_bf16_kernel<320,256,2,4>";
+    case KERN_128x128: return "gemm_bf16_kernel<128,128,2,2>";
+    default: return "gemm_bf16_kernel<256,128,4,2>";
   }
-  if (N % 256 == 0 && fam == 0) {
-    const bool ph8 = prefer_8ph(M, N);
-    if (prefer_small(M, N, ph8)) return "gemm_bf16_kernel<128,128,2,2>";
-    if (ph8) return "gemm_bf16_8ph_kernel<256,256>";
-  }
-  if (fam == 9) return "gemm_bf16_kernel<128,128,2,2>";
-  return N % 256 == 0 ? "gemm_bf16_kernel<320,256,2,4>" : "gemm_bf16_kernel<256,128,4,2>";
 }
 
 extern "C" int aaclip_gemm_pin(int in_dtype, int M, int N, int K, int family) {
   AACLIP_REQUIRE((in_dtype == AACLIP_BF16 || in_dtype == AACLIP_F16) && M > 0 && N > 0 && K > 0);
   AACLIP_REQUIRE(family == 0 || family == 1 || family == 2 || family == 3 || family == 8 || family == 9);
   AACLIP_REQUIRE(family == 0 || family == 2 || N % 256 == 0);
-  for (int i = 0; i < g_npins; ++i)
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  const int n = g_npins.load(std::memory_order_relaxed);
+  for (int i = 0; i < n; ++i)
     if (g_pins[i].dtype == in_dtype && g_pins[i].M == M && g_pins[i].N == N && g_pins[i].K == K) {
-      g_pins[i].fam = family;
+      if (family) {
+        g_pins[i].fam = family;
+      } else {  // unpin: move the last entry into the hole
+        g_pins[i] = g_pins[n - 1];
+        g_npins.store(n - 1, std::memory_order_release);
+      }
       return AACLIP_OK;
     }
   if (family == 0) return AACLIP_OK;
-  AACLIP_REQUIRE(g_npins < kPins);
-  g_pins[g_npins++] = Pin{in_dtype, M, N, K, family};
+  AACLIP_REQUIRE(n < kPins);
+  g_pins[n] = Pin{in_dtype, M, N, K, family};
+  g_npins.store(n + 1, std::memory_order_release);
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_gemm_concurrent(int on, int* previous) {
+  AACLIP_REQUIRE(on == 0 || on == 1);
+  if (previous) *previous = t_concurrent;
+  t_concurrent = on;
   return AACLIP_OK;
 }
 

@@ -142,12 +142,24 @@ int aaclip_set_gemm_variant(int variant);
  * 1 = 256x256, 2 = 256x128, 3 = 256x256 8-phase ping-pong, 8 = 320x256,
  * 9 = 128x128, 0 = unpin (back to the heuristic). Set by a measuring tuner at
  * engine setup (aaclip/ops.py tune_gemm); every family accumulates K in the same
- * order, so a pin changes speed, never bits. Process-global, host only.
+ * order, so a pin changes speed, never bits. Process-global (mutex-guarded), host
+ * only; unpinning removes the entry, so at most 256 shapes are pinned at once.
  */
 int aaclip_gemm_pin(int in_dtype, int M, int N, int K, int family);
 
-/* Name of the kernel aaclip_gemm launches for (in_dtype, M, N, K) under the current
- * variant (the default dispatch's per-shape choice). Host only, for reports. */
+/*
+ * Concurrent-chunk mode for the CALLING HOST THREAD (on = 1 / 0; *previous, if
+ * non-null, receives the old state): while set, 16-bit GEMMs whose 256x256 tiles fill
+ * at least one round of the CUs launch the 8-phase kernel (the other stream's chunk
+ * fills the partial last round). Set by VisualEngine.predict around the enqueue of
+ * concurrent image chunks (graph capture included: the choice is made at launch).
+ * Pins and the variant hook take precedence. Same K order, so bits are unchanged.
+ */
+int aaclip_gemm_concurrent(int on, int* previous);
+
+/* Name of the kernel aaclip_gemm launches for (in_dtype, M, N, K) with lda = ldw = K,
+ * on the calling thread, under the current variant / pins / concurrent mode (the
+ * dispatch's own decision). Host only, for reports. */
 const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K);
 
 /*

@@ -80,3 +80,51 @@ def test_gemm_plan_per_shape_choice():
     assert [plan(4616, n) for n in (3072, 1024, 4096)] == [ph8, small, t320]
     assert plan(100, 384) == "gemm_bf16_kernel<256,128,4,2>"
     assert lib.aaclip_gemm_plan(_lib.F32, 100, 256, 64) == b"gemm_f32_kernel"
+
+
+def test_gemm_pin_table_unpins_and_never_fills():
+    """aaclip_gemm_pin: unpinning removes the entry, so pinning and unpinning far more
+    distinct shapes than the table holds (256) never fails; pins override the
+    heuristic and their removal restores it (host logic, no launch)."""
+    lib = _lib.lib()
+    ph8, t320 = "gemm_bf16_8ph_kernel<256,256>", "gemm_bf16_kernel<320,256,2,4>"
+    plan = lambda M, N, K=1024: lib.aaclip_gemm_plan(_lib.BF16, M, N, K).decode()  # noqa: E731
+    for rnd in range(3):
+        for b in range(1, 301):  # 300 distinct chunk sizes per round
+            assert lib.aaclip_gemm_pin(_lib.BF16, b * 577, 4096, 1024, 8) == 0
+            assert plan(b * 577, 4096) == t320
+            assert lib.aaclip_gemm_pin(_lib.BF16, b * 577, 4096, 1024, 0) == 0
+    assert plan(18464, 3072) == ph8  # heuristic again
+    # many live pins at once: the table's capacity is reported as an argument error, not UB
+    before = plan(1000, 1024)
+    rc = [lib.aaclip_gemm_pin(_lib.BF16, 1000 + i, 1024, 1024, 8) for i in range(300)]
+    assert rc[:256] == [0] * 256 and set(rc[256:]) == {1}
+    for i in range(300):
+        assert lib.aaclip_gemm_pin(_lib.BF16, 1000 + i, 1024, 1024, 0) == 0
+    assert plan(1000, 1024) == before != t320  # no stale entry left behind
+    assert lib.aaclip_gemm_pin(_lib.BF16, 1000, 1024, 1024, 9) == 0
+    assert plan(1000, 1024) == "gemm_bf16_kernel<128,128,2,2>"
+    assert lib.aaclip_gemm_pin(_lib.BF16, 1000, 1024, 1024, 0) == 0
+
+
+def test_gemm_concurrent_mode_is_thread_local():
+    """aaclip_gemm_concurrent: on the calling thread, shapes whose 256x256 tiles fill a
+    round of the 256 CUs take the 8-phase kernel (c_fc at 16 images per chunk), other
+    threads keep the heuristic, and the previous state comes back."""
+    import threading
+    from aaclip import ops
+    lib = _lib.lib()
+    ph8, t320 = "gemm_bf16_8ph_kernel<256,256>", "gemm_bf16_kernel<320,256,2,4>"
+    plan = lambda: lib.aaclip_gemm_plan(_lib.BF16, 9232, 4096, 1024).decode()  # noqa: E731
+    assert plan() == t320
+    seen = {}
+    with ops.concurrent_gemms(True):
+        assert plan() == ph8
+        assert lib.aaclip_gemm_plan(_lib.BF16, 577, 4096, 1024).decode() != ph8  # under one round: unchanged
+        t = threading.Thread(target=lambda: seen.setdefault("other", plan()))
+        t.start()
+        t.join()
+        with ops.concurrent_gemms(False):
+            assert plan() == t320
+        assert plan() == ph8
+    assert plan() == t320 and seen["other"] == t320

@@ -208,7 +208,7 @@ def test_f16_batch_composition_invariance(dev, weights):
 
 def test_concurrent_chunk_pins(dev, weights):
     """Two 16-image chunks on two streams pin the 8-phase GEMM for their wide block
-    shapes while they are enqueued (VisualEngine._concurrent_pins): the maps and scores
+    shapes while they are enqueued (aaclip_gemm_concurrent, thread-local): the maps and scores
     are bit-identical to one stream (same K order), and the heuristic is back afterwards."""
     from aaclip import _lib
     eng = VisualEngine(*weights, dtype=H16)
