@@ -54,6 +54,28 @@ def _dev(*ts):
                                "wrap the call in torch.cuda.device(...)")
 
 
+# In-step launch probe (measurement only; None in production): an object with
+# begin(kind, name, flops, nbytes) -> token and end(token), called around every
+# launch of the ops below so a caller (bench.py) can put HIP timing events around
+# each kernel inside a captured step. It never changes what is launched.
+_probe = None
+
+
+def set_probe(probe) -> None:
+    global _probe
+    _probe = probe
+
+
+def _launch(kind: str, name, flops: float, nbytes: float, fn, *args) -> None:
+    """call(fn, *args), bracketed by the probe when one is set."""
+    if _probe is None:
+        call(fn, *args)
+        return
+    tok = _probe.begin(kind, name() if callable(name) else name, flops, nbytes)
+    call(fn, *args)
+    _probe.end(tok)
+
+
 def _rowmajor(t: torch.Tensor, name: str):
     if t.dim() != 2 or t.stride(1) != 1:
         raise ValueError(f"{name} must be a 2-D tensor with unit column stride")
@@ -79,9 +101,12 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
         raise ValueError("gemm output rows too small for the row remap")
     epi, ldr, ldaux = _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux,
                                       aux_dtype=torch.float16 if a.dtype == torch.float16 else torch.bfloat16)
-    call("aaclip_gemm", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w), w.stride(0),
-         _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
-         row_group, row_group_out, row_offset, _stream())
+    kind = f"gemm N{N} K{K}" + (" leaky" if leaky else "") + (" gelu" if gelu else "") + (" resid" if residual is not None else "")
+    nbytes = (M * K + N * K) * a.element_size() + rows_out * N * out.element_size() * (2 if residual is not None else 1)
+    _launch(kind, lambda: gemm_plan(dtag(a), M, N, K) if a.dtype != torch.float32 else "gemm_f32_kernel",
+            2.0 * M * N * K, nbytes, "aaclip_gemm", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w),
+            w.stride(0), _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
+            row_group, row_group_out, row_offset, _stream())
     return out
 
 
@@ -298,8 +323,10 @@ def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads:
         return out
     if qkv.dtype != out.dtype:
         raise ValueError("attention tensors must share a dtype")
-    call("aaclip_attention", dtag(qkv), _ptr(qkv), _ptr(out), batch, seq, heads, hd, flags, None, 0,
-         _stream())
+    flops = 4.0 * batch * heads * seq * seq * hd / (2 if causal else 1)
+    _launch("attention", {torch.float32: "attn_f32_kernel"}.get(qkv.dtype, "attn_bf16_kernel"), flops,
+            qkv.numel() * qkv.element_size() + out.numel() * out.element_size(), "aaclip_attention", dtag(qkv),
+            _ptr(qkv), _ptr(out), batch, seq, heads, hd, flags, None, 0, _stream())
     return out
 
 
@@ -312,7 +339,8 @@ def im2col(img: torch.Tensor, cols: torch.Tensor, patch: int) -> torch.Tensor:
         raise ValueError("image must be contiguous fp32 [B,C,S,S]")
     if cols.shape[0] != B * g * g or not cols.is_contiguous():
         raise ValueError("cols shape mismatch")
-    call("aaclip_im2col", dtag(cols), _ptr(img), _ptr(cols), B, C, S, patch, cols.shape[1], _stream())
+    _launch("im2col", "im2col_kernel", 0.0, img.numel() * 4 + cols.numel() * cols.element_size(), "aaclip_im2col",
+            dtag(cols), _ptr(img), _ptr(cols), B, C, S, patch, cols.shape[1], _stream())
     return cols
 
 
@@ -331,8 +359,9 @@ def embed_ln(x, cls, pos, ln_pre, ln1, h, batch, n_tok, h_sc=None):
     if x.shape[0] != batch * n_tok or h.shape != x.shape or pos.shape != (n_tok, width):
         raise ValueError("embed_ln shape mismatch")
     od, scp, ld = _mx_out(h, h_sc, x.shape[0])
-    call("aaclip_embed_ln", od, _ptr(x), _ptr(cls), _ptr(pos), _ptr(ln_pre[0]), _ptr(ln_pre[1]),
-         _ptr(ln1[0]), _ptr(ln1[1]), _ptr(h), batch, n_tok, width, scp, ld, _stream())
+    _launch("embed_ln", "embed_ln_kernel", 0.0, x.numel() * 4 * 2 + h.numel() * h.element_size(), "aaclip_embed_ln",
+            od, _ptr(x), _ptr(cls), _ptr(pos), _ptr(ln_pre[0]), _ptr(ln_pre[1]), _ptr(ln1[0]), _ptr(ln1[1]),
+            _ptr(h), batch, n_tok, width, scp, ld, _stream())
 
 
 def block_tail(x, n_tok, *, u=None, adapt_weight=0.0, ln=None, h=None, post=None, tap=None, out_dtype=None,
@@ -350,7 +379,9 @@ def block_tail(x, n_tok, *, u=None, adapt_weight=0.0, ln=None, h=None, post=None
         od = dtag(tap) if tap is not None else F32
     if h is not None and tap is not None and h.dtype != tap.dtype and not (h.dtype == FP8 and tap.dtype == torch.bfloat16):
         raise ValueError("h and tap must share a dtype (or h fp8 MX with bf16 taps)")
-    call("aaclip_block_tail", od, _ptr(x), _ptr(u), float(adapt_weight),
+    nb = rows * width * 4 * (3 if u is not None else 2) + (rows * width * h.element_size() if h is not None else 0) \
+        + (tap.numel() * tap.element_size() if tap is not None else 0)
+    _launch("block_tail", "block_tail_kernel", 0.0, nb, "aaclip_block_tail", od, _ptr(x), _ptr(u), float(adapt_weight),
          _ptr(ln[0]) if ln else None, _ptr(ln[1]) if ln else None, _ptr(h),
          _ptr(post[0]) if post else None, _ptr(post[1]) if post else None, _ptr(tap),
          rows, n_tok, width, scp, ld, _stream())
@@ -363,8 +394,9 @@ def layernorm(x, w, b, y, y_sc=None):
     if x.shape != y.shape or x.dtype != torch.float32:
         raise ValueError("layernorm shape/dtype mismatch")
     od, scp, ld = _mx_out(y, y_sc, x.shape[0])
-    call("aaclip_layernorm", od, _ptr(x), x.stride(0), _ptr(w), _ptr(b), _ptr(y), y.stride(0),
-         x.shape[0], x.shape[1], scp, ld, _stream())
+    _launch("layernorm", "layernorm_kernel", 0.0, x.numel() * 4 + y.numel() * y.element_size(), "aaclip_layernorm",
+            od, _ptr(x), x.stride(0), _ptr(w), _ptr(b), _ptr(y), y.stride(0), x.shape[0], x.shape[1], scp, ld,
+            _stream())
     return y
 
 
@@ -470,8 +502,10 @@ def anomaly_map(levels, T, out, grid_ws, *, g, ksize, sigma, normalize=True):
         if t.shape != (rows, C) or t.stride(0) != levels[0].stride(0) or t.dtype != levels[0].dtype:
             raise ValueError("levels must share shape, dtype and stride")
     arr = _level_array(levels)
-    call("aaclip_anomaly_map", dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(T), B, g, C,
-         int(normalize), S, ksize, float(sigma), _ptr(grid_ws), _ptr(out), _stream())
+    nb = len(levels) * rows * C * levels[0].element_size() + C * 2 * 4 + B * S * S * 4 + 2 * rows * 4
+    _launch("anomaly_map", "anomaly_map (patch_scores + blur_upsample)", 0.0, nb, "aaclip_anomaly_map",
+            dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(T), B, g, C, int(normalize), S, ksize,
+            float(sigma), _ptr(grid_ws), _ptr(out), _stream())
     return out
 
 
@@ -481,8 +515,9 @@ def image_score(det_raw, batch, n_patch, partial, det=None, T=None, score=None, 
     rows, C = det_raw.shape
     if rows != batch * n_patch or partial.numel() < batch * ((n_patch + 63) // 64) * C:
         raise ValueError("image_score shape mismatch")
-    call("aaclip_image_score", dtag(det_raw), _ptr(det_raw), det_raw.stride(0), _ptr(T), batch, n_patch, C,
-         int(normalize), _ptr(partial), _ptr(det), _ptr(score), _stream())
+    _launch("image_score", "image_score (det_partial + det_finalize)", 0.0, rows * C * det_raw.element_size(),
+            "aaclip_image_score", dtag(det_raw), _ptr(det_raw), det_raw.stride(0), _ptr(T), batch, n_patch, C,
+            int(normalize), _ptr(partial), _ptr(det), _ptr(score), _stream())
 
 
 def metrics_eval(pixel_preds: torch.Tensor, pixel_label: torch.Tensor, image_preds: torch.Tensor,

@@ -52,3 +52,30 @@ def sharded_step(predict, x_local: torch.Tensor, T: torch.Tensor, n_total: int, 
     s_all = gather_rows(scores, n_total, group)
     m_all = gather_rows(maps, n_total, group) if gather_maps else None
     return maps, scores, s_all, m_all
+
+
+def verify_gather(predict, images_of, s_all: torch.Tensor, s_local: torch.Tensor, n_total: int, group=None,
+                  checker: int = 0) -> dict:
+    """Self-check of a data-parallel step after the fact, so an N-rank run proves its
+    own gathered result: (1) every rank finds its local scores, bit for bit, at its
+    shard_range slice of the gathered vector; (2) rank `checker` recomputes the shard of
+    the LAST rank (a foreign shard it never predicted in the step) with
+    `predict(images_of(a, b))` and compares it bit for bit with that slice. Per-image
+    results do not depend on batch composition (tests/test_e2e_gpu.py), so the foreign
+    shard's bits are the same whoever computes them. Both flags are MIN-reduced over
+    the ranks, so every rank returns the same verdict:
+    {"backend", "world", "own_slice_verified", "gather_verified", "checked_shard"}."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    a, b = shard_range(n_total, rank, world)
+    own = bool(torch.equal(s_all[a:b], s_local))
+    foreign = True
+    fa, fb = shard_range(n_total, world - 1, world)
+    if rank == checker and fb > fa:
+        ref = predict(images_of(fa, fb))
+        foreign = bool(torch.equal(s_all[fa:fb], ref.to(s_all.device)))
+    flags = torch.tensor([int(own), int(foreign)], dtype=torch.int32, device=s_all.device)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN, group=group)
+    return {"backend": str(dist.get_backend(group)), "world": world, "own_slice_verified": bool(flags[0]),
+            "gather_verified": bool(flags[1]), "checked_shard": {"rank": world - 1, "images": [fa, fb],
+                                                                 "checked_by": checker}}

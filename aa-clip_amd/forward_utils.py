@@ -90,6 +90,8 @@ def calculate_similarity_map(patch_features, epoch_text_feature, img_size, test=
     Cn = epoch_text_feature.shape[1]
     if test:
         assert Cn == 2
+    elif not 1 <= Cn <= 8:  # checked before any launch: the train-branch upsample holds <= 8 channels per pixel
+        raise ValueError(f"train-branch similarity map supports 1..8 anchors, got {Cn}")
     f = patch_features.reshape(B * L, C)
     if f.dtype not in (torch.float32, torch.bfloat16):
         f = f.float()
@@ -124,42 +126,22 @@ def anomaly_map_multilevel(patch_features, epoch_text_feature, img_size, domain=
 
 
 def metrics_eval(pixel_label, image_label, pixel_preds, image_preds, class_names: str, domain: str):
-    """forward_utils.py:233-280. Tensors (or numpy arrays, when a GPU is present)
-    go through the device kernel; the rounding / dict layout are the reference's."""
-    tensors = any(isinstance(t, torch.Tensor) for t in (pixel_label, image_label, pixel_preds, image_preds))
-    if tensors or torch.cuda.is_available():
-        dev = next((t.device for t in (pixel_preds, pixel_label) if isinstance(t, torch.Tensor) and t.is_cuda),
-                   torch.device("cuda", torch.cuda.current_device()))
-        t = [x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x))
-             for x in (pixel_preds, pixel_label, image_preds, image_label)]
-        t = [x.to(dev, non_blocking=True) for x in t]
-        pauc, pap, iauc, iap = ops.metrics_eval(t[0], t[1], t[2], t[3], medical=(domain == "Medical"))
-        if pauc != pauc:  # NaN: one pixel class only, sklearn raises here
-            raise ValueError("Only one class present in y_true. ROC AUC score is not defined in that case.")
-    else:
-        pauc, pap, iauc, iap = _metrics_host(pixel_label, image_label, pixel_preds, image_preds, domain)
+    """forward_utils.py:233-280 on the device (aaclip_metrics_eval: class min-max, score
+    fusion, exact tie-aware AUROC / AP). Tensors or numpy arrays; the rounding and the
+    dict layout are the reference's. There is no CPU path: without a GPU this raises."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("metrics_eval runs on the MI355X kernels (aaclip_metrics_eval); no GPU is visible "
+                           "and there is no CPU path")
+    dev = next((t.device for t in (pixel_preds, pixel_label) if isinstance(t, torch.Tensor) and t.is_cuda),
+               torch.device("cuda", torch.cuda.current_device()))
+    t = [x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x))
+         for x in (pixel_preds, pixel_label, image_preds, image_label)]
+    t = [x.to(dev, non_blocking=True) for x in t]
+    pauc, pap, iauc, iap = ops.metrics_eval(t[0], t[1], t[2], t[3], medical=(domain == "Medical"))
+    if pauc != pauc:  # NaN: one pixel class only, sklearn raises here
+        raise ValueError("Only one class present in y_true. ROC AUC score is not defined in that case.")
     return {"class name": class_names, "pixel AUC": round(pauc, 4) * 100, "pixel AP": round(pap, 4) * 100,
             "image AUC": round(iauc, 4) * 100, "image AP": round(iap, 4) * 100}
-
-
-def _metrics_host(pixel_label, image_label, pixel_preds, image_preds, domain):
-    """numpy/sklearn formulation of the reference (forward_utils.py:241-271), for
-    numpy inputs on a host without a GPU."""
-    from sklearn.metrics import average_precision_score, roc_auc_score
-    if pixel_preds.max() != 1:
-        pixel_preds = (pixel_preds - pixel_preds.min()) / (pixel_preds.max() - pixel_preds.min())
-    if image_preds.max() != 1:
-        image_preds = (image_preds - image_preds.min()) / (image_preds.max() - image_preds.min())
-    pmax = pixel_preds.max(axis=(1, 2))
-    image_preds = pmax if domain == "Medical" else pmax * 0.5 + image_preds * 0.5
-    y, s = pixel_label.flatten(), pixel_preds.flatten()
-    pauc, pap = roc_auc_score(y, s), average_precision_score(y, s)
-    if image_label.max() != image_label.min():
-        iauc = roc_auc_score(image_label.flatten(), image_preds.flatten())
-        iap = average_precision_score(image_label.flatten(), image_preds.flatten())
-    else:
-        iauc = iap = 0
-    return pauc, pap, iauc, iap
 
 
 def visualize(pixel_label, pixel_preds, file_names, save_dir, dataset_name, class_name):

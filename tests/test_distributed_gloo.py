@@ -85,7 +85,15 @@ def _sharded_worker(rank, world, port, n, q):
     g = torch.Generator().manual_seed(111)
     x_global = torch.randn(n, 3, 28, 28, generator=g)
     a, b = shard_range(n, rank, world)
-    _, _, s_all, m_all = sharded_step(model.predict, x_global[a:b], T, n, gather_maps=True)
+    _, s_loc, s_all, m_all = sharded_step(model.predict, x_global[a:b], T, n, gather_maps=True)
+    # the bench's N-rank self-check: own slices + the last rank's shard recomputed on rank 0
+    from aaclip.parallel import verify_gather
+    pred = lambda xi: model.predict(xi, T)[1]  # noqa: E731
+    check = verify_gather(pred, lambda i0, i1: x_global[i0:i1], s_all, s_loc, n)
+    bad = s_all.clone()
+    fa, fb = shard_range(n, world - 1, world)
+    bad[fb - 1] += 1.0  # a corrupted gather (last image of the foreign shard) must be caught
+    check_bad = verify_gather(pred, lambda i0, i1: x_global[i0:i1], bad, s_loc, n)
     # harness: one class's dataset sharded by image, gathered before metrics
     ds = get_dataset("synthetic", 28, None, -1, "test", synthetic_n=n)["bottle"]
     sub = torch.utils.data.Subset(ds, range(*shard_range(n, rank, world)))
@@ -93,7 +101,7 @@ def _sharded_worker(rank, world, port, n, q):
     masks, labels, preds, preds_image, names = harness.get_predictions(model, T, loader, torch.device("cpu"), 28,
                                                                        dataset="synthetic", n_total=n)
     q.put((rank, s_all.tolist(), m_all.sum().item(), masks.sum(), labels.tolist(), preds.sum().item(),
-           preds_image.tolist(), names))
+           preds_image.tolist(), names, check, check_bad))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -126,7 +134,11 @@ def test_gloo_world2_sharded_step_and_harness(n):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for _, s_all, m_sum, mk_sum, labels, p_sum, pi, names in out:
+    for _, s_all, m_sum, mk_sum, labels, p_sum, pi, names, check, check_bad in out:
+        assert check["backend"] == "gloo" and check["world"] == 2
+        assert check["gather_verified"] and check["own_slice_verified"], check
+        # the corruption sits in the last rank's own slice and in the foreign shard rank 0 checks
+        assert not check_bad["gather_verified"] and not check_bad["own_slice_verified"], check_bad
         assert s_all == ref_scores.tolist()
         assert m_sum == ref_maps.sum().item()
         assert mk_sum == ref[0].sum() and labels == ref[1].tolist()

@@ -71,6 +71,10 @@ def test_visual_bf16_parity(dev, golden, weights):
     r = _check_e2e(eng, golden, dev, (1e-3, 1e-2))
     print("bf16:", r)
     assert r["map_ok"], r
+    # bf16 operands (8 significant bits) can flip a patch label whose margin is within
+    # their rounding: reported, and held to a regression bound (the contract mode,
+    # fp16, has 0: tests/test_fp16_gpu.py)
+    assert r["flips_sure"] <= 0.01 * r["n_sure"], r
     e = golden["e2e"]
     x = torch.from_numpy(synth.images(111, 2, 336)).to(dev)
     T = torch.from_numpy(e["T"]).to(dev)
@@ -228,10 +232,18 @@ def test_518_default_size_parity(dev, dtype):
             else:
                 assert (err <= 1e-3 + 1e-2 * np.abs(ref)).all()
         np.testing.assert_allclose(score.cpu().numpy(), g["score"], atol=1e-4 if dtype != torch.bfloat16 else 1e-3)
+    # patch labels (argmax over the 2 anchors per level and patch) where the reference's
+    # margin exceeds 1e-3 on the x100 scale: exact in fp32 and fp16 (the contract mode),
+    # reported and bounded in bf16
+    seg, det = eng.forward(x)
+    grid = np.stack([(100.0 * (f @ T)).cpu().numpy() for f in seg], axis=1)
+    ref = g["grid_A"]
+    sure = np.abs(ref[..., 1] - ref[..., 0]) > 1e-3
+    flips = int((grid.argmax(-1) != ref.argmax(-1))[sure].sum())
+    print(dtype, f"518 patch-label flips (sure) {flips}/{int(sure.sum())}")
+    if dtype == torch.bfloat16:
+        assert flips <= 0.01 * sure.sum()
+    else:
+        assert flips == 0
     if dtype == torch.float32:
-        seg, det = eng.forward(x)
-        grid = np.stack([(100.0 * (f @ T)).cpu().numpy() for f in seg], axis=1)
-        ref = g["grid_A"]
-        sure = np.abs(ref[..., 1] - ref[..., 0]) > 1e-3
-        assert int((grid.argmax(-1) != ref.argmax(-1))[sure].sum()) == 0
         np.testing.assert_allclose(grid, ref, atol=5e-3)

@@ -191,6 +191,13 @@ def test_visual_f16_c5_golden(dev, golden):
     print("fp16 c5 map max abs err", err.max())
     assert (err <= 1e-3 + 1e-2 * np.abs(ref)).all()
     np.testing.assert_allclose(score.cpu().numpy(), g["score"], atol=2e-4)
+    # patch labels over all 6 levels x 1024 patches: exact where the reference's margin > 1e-3
+    seg, _ = eng.forward(x)
+    grid = np.stack([(100.0 * (f @ T)).cpu().numpy() for f in seg], axis=1)
+    sure = np.abs(g["grid_A"][..., 1] - g["grid_A"][..., 0]) > 1e-3
+    flips = int((grid.argmax(-1) != g["grid_A"].argmax(-1))[sure].sum())
+    print(f"fp16 c5 patch-label flips (sure) {flips}/{int(sure.sum())}")
+    assert flips == 0
 
 
 def test_f16_batch_composition_invariance(dev, weights):

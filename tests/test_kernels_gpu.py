@@ -473,3 +473,56 @@ def test_anomaly_map_equals_stages(dev, dt, B, g, S, L, dom):
         out = torch.full((B, S, S), float("nan"), device=dev)
         ops.anomaly_map(lv, T, out, ws, g=g, ksize=k, sigma=s)
         assert torch.equal(out, ref[:, 0])
+
+
+# ----------------------------------------------------------------------------- NaN propagation
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("where", ["q", "k", "v"])
+def test_attention_nan_propagates_like_reference(dev, dt, where):
+    """A NaN in the packed qkv (e.g. an upstream fp16 overflow) reaches exactly the
+    outputs it reaches in the reference's softmax(q k^T) v: a NaN in one query row ->
+    that row of that head; in one key or value row -> every query of that head (N = 577
+    with its key tail, 16 heads). The attention TU is built with -fno-honor-nans for its
+    score max: this screens that the flag never turns a NaN into a finite output, and
+    that the other heads and rows are unaffected."""
+    B, N, H = 2, 577, 16
+    torch.manual_seed(5)
+    qkv = (torch.randn(B * N, 3 * H * 64, device=dev) * 1.5).to(dt)
+    col = {"q": 0, "k": H * 64, "v": 2 * H * 64}[where] + 3 * 64 + 7  # head 3, dim 7
+    row = 1 * N + 200  # image 1, token 200
+    qkv[row, col] = float("nan")
+    out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
+    ops.attention(qkv, out, B, N, H)
+    ref = _attn_ref(qkv, B, N, H, False)
+    assert torch.equal(torch.isnan(out), torch.isnan(ref)), (where, int(torch.isnan(out).sum()),
+                                                             int(torch.isnan(ref).sum()))
+    fin = ~torch.isnan(ref)
+    assert (out.double()[fin] - ref[fin]).abs().max().item() < (3e-2 if dt == torch.bfloat16 else 4e-3)
+
+
+# ----------------------------------------------------------------------------- train-branch map, any anchor count
+@pytest.mark.parametrize("Cn", [1, 3, 8])
+def test_similarity_map_train_any_anchor_count(dev, Cn):
+    """forward_utils.calculate_similarity_map(test=False) for 1, 3 and 8 anchors at 518 px
+    (37x37 grid): 100 f.T -> [B, Cn, g, g] -> bilinear align_corners=True to S x S ->
+    softmax over the anchors when Cn > 1 (reference forward_utils.py:199-215), against
+    the same formula in fp64 torch."""
+    from forward_utils import calculate_similarity_map
+    B, g, S = 2, 37, 518
+    torch.manual_seed(Cn)
+    f = torch.nn.functional.normalize(torch.randn(B, g * g, 768, device=dev), dim=-1)
+    T = torch.nn.functional.normalize(torch.randn(768, Cn, device=dev), dim=0)
+    got = calculate_similarity_map(f, T, S, test=False)
+    A = (100.0 * (f.double() @ T.double())).permute(0, 2, 1).reshape(B, Cn, g, g)
+    ref = torch.nn.functional.interpolate(A, size=(S, S), mode="bilinear", align_corners=True)
+    if Cn > 1:
+        ref = torch.softmax(ref, dim=1)
+    assert got.shape == (B, Cn, S, S)
+    assert (got.double() - ref).abs().max().item() < (2e-5 if Cn > 1 else 2e-4)
+
+
+def test_similarity_map_train_rejects_too_many_anchors_before_launch(dev):
+    from forward_utils import calculate_similarity_map
+    f = torch.randn(1, 24 * 24, 768, device=dev)
+    with pytest.raises(ValueError):
+        calculate_similarity_map(f, torch.randn(768, 9, device=dev), 336, test=False)

@@ -121,3 +121,16 @@ def test_metrics_ragged_pixel_counts(dev, N, S):
     got = _dev_metrics(dev, masks, labels, pp, ip, "Industrial")
     want = _sk(masks, labels, pp.copy(), ip.copy(), "Industrial")
     assert np.allclose(got, want, rtol=0, atol=1e-9), (got, want)
+
+
+def test_forward_utils_metrics_golden(dev, golden):
+    """The drop-in metrics_eval vs the reference's own metrics_eval output (golden_ops:
+    forward_utils.py:233-280 run by tests/golden/make_golden.py), both domains."""
+    import json
+    from forward_utils import metrics_eval
+    o = golden["ops"]
+    ref = json.loads(str(o["met_result"]))
+    for dom in ("Industrial", "Medical"):
+        r = metrics_eval(o["met_masks"], o["met_labels"], o["met_pp"].copy(), o["met_ip"].copy(), "synthetic", dom)
+        for k in ("pixel AUC", "pixel AP", "image AUC", "image AP"):
+            assert r[k] == pytest.approx(ref[dom][k], abs=1e-9)
