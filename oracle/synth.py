@@ -182,6 +182,51 @@ def write_openai_checkpoint(path: str, seed: int = 111) -> None:
     torch.save(out, path)
 
 
+def _torchscript_holder(tensors: dict):
+    """A module tree whose state_dict() keys are exactly `tensors`' dotted names (floating
+    tensors as parameters, the rest as buffers), scriptable: the shape of the OpenAI
+    release archive's module (reference model/openai.py:56-59 reads it with
+    torch.jit.load(...).state_dict())."""
+    import torch
+    from torch import nn
+
+    class Holder(nn.Module):
+        def forward(self, x: torch.Tensor) -> torch.Tensor:
+            return x
+
+    root = Holder()
+    for k, v in tensors.items():
+        parts = k.split(".")
+        m = root
+        for p in parts[:-1]:
+            if p not in m._modules:
+                m.add_module(p, Holder())
+            m = m._modules[p]
+        if v.is_floating_point():
+            m.register_parameter(parts[-1], nn.Parameter(v, requires_grad=False))
+        else:
+            m.register_buffer(parts[-1], v)
+    return root
+
+
+def write_openai_torchscript(path: str, seed: int = 111) -> None:
+    """The same synthetic checkpoint as write_openai_checkpoint, in the OpenAI RELEASE
+    format: a TorchScript archive (torch.jit.save of a scripted module holding the
+    tensors; fp16 where OpenAI's convert_weights casts, metadata entries as buffers).
+    The reference's loader takes its torch.jit.load branch on it (model/openai.py:56-59,
+    then build_model_from_openai_state_dict(model.state_dict()))."""
+    import torch
+    sd = clip_state_dict(seed)
+    tensors = {}
+    for k, v in sd.items():
+        t = torch.from_numpy(np.ascontiguousarray(v))
+        tensors[k] = t.half() if k.endswith(_OPENAI_FP16) else t
+    tensors["input_resolution"] = torch.tensor(336)
+    tensors["context_length"] = torch.tensor(CONTEXT)
+    tensors["vocab_size"] = torch.tensor(VOCAB)
+    torch.jit.save(torch.jit.script(_torchscript_holder(tensors)), path)
+
+
 def torch_state_checksum(sd) -> str:
     """SHA-256 over a torch state dict's floating tensors as float32 (sorted keys)."""
     h = hashlib.sha256()
