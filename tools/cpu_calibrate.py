@@ -10,7 +10,9 @@ tests/golden/make_golden.py):
 
 Per leg: bs = 1 images at 336 px through forward + 4-level anomaly map + image
 score (reference: AdaptedCLIP.forward, calculate_similarity_map per level, the
-test.py:83-93 sum and score), 2 warm-up images, then >= --seconds of steady state.
+test.py:83-93 sum and score), 2 warm-up images, then the reference and the torch port
+alternate in 3 slices each (2 x --seconds per candidate in all); the numpy port once.
+Run it on an otherwise idle host: anything else on the cores skews the ratio.
 Writes profiles/r03/cpu_calibration.json.
 """
 from __future__ import annotations
@@ -91,16 +93,32 @@ def main():
         t_map = RT.anomaly_map(s2, Tt, 336, "Industrial").numpy()
     out = {"host": {"nproc": os.cpu_count(), "torch": torch.__version__, "numpy": np.__version__},
            "workload": "bs=1 synthetic 336 px images, forward + 4-level anomaly map + image score, fp32; "
-                       "2 warm-up images then >= %.0f s steady state per leg" % args.seconds,
+                       "2 warm-up images each, then reference and torch port alternating in 3 slices "
+                       "(%.0f s each in all), numpy port %.0f s" % (2 * args.seconds, args.seconds / 2),
            "map_max_abs_diff_vs_reference": {"numpy_port": float(np.abs(np_map - ref_map).max()),
                                              "torch_port": float(np.abs(t_map - ref_map).max())},
            "legs": {}}
+
+    def interleaved(fns, seconds, rounds=3):
+        """Alternate the candidates in `rounds` slices of seconds/rounds each (slow drift
+        in the host's clock or load then hits all of them alike)."""
+        tot = {k: [0, 0.0] for k in fns}
+        for k, f in fns.items():  # warm-up
+            for i in range(2):
+                f(i % pool)
+        for r in range(rounds):
+            for k, f in fns.items():
+                leg = _legs(f, pool, seconds / rounds, warmup=0)
+                tot[k][0] += leg["images"]
+                tot[k][1] += leg["seconds"]
+        return {k: {"images_per_sec": round(n / t, 4), "images": n, "seconds": round(t, 2)} for k, (n, t) in
+                tot.items()}
+
     for th in [int(v) for v in args.threads.split(",")]:
         torch.set_num_threads(th)
         with threadpool_limits(limits=th):
-            leg = {"reference": _legs(ref_one, pool, args.seconds),
-                   "numpy_port": _legs(np_one, pool, args.seconds),
-                   "torch_port": _legs(torch_one, pool, args.seconds)}
+            leg = interleaved({"reference": ref_one, "torch_port": torch_one}, 2 * args.seconds)
+            leg["numpy_port"] = _legs(np_one, pool, args.seconds / 2)
         r = leg["reference"]["images_per_sec"]
         leg["ratio_numpy_port_over_reference"] = round(leg["numpy_port"]["images_per_sec"] / r, 4)
         leg["ratio_torch_port_over_reference"] = round(leg["torch_port"]["images_per_sec"] / r, 4)
