@@ -157,6 +157,7 @@ class VisualEngine:
         self.relu = r_det
         self.w_seg = [cdt(t) for t in self.w_seg[:-1]] + [cdt(torch.cat([self.w_seg[-1], w_det], 0))]
         self._ws = {}
+        self.poison = False  # tests: fill new workspaces with NaN (read-before-write screen)
 
     # ------------------------------------------------------------------ workspace
     def _workspace(self, B: int, S: int, slot: int = 0):
@@ -193,7 +194,7 @@ class VisualEngine:
             asc=ops.mx_scales(R, WIDTH, dev) if self.fp8 else None,
             f8=e(R, 4 * WIDTH, dt=FP8) if self.fp8 else None,
             fsc=ops.mx_scales(R, 4 * WIDTH, dev) if self.fp8 else None,
-            grid=e(B * P, dt=torch.float32), partial=e(B * ((P + 63) // 64) * EMBED, dt=torch.float32),
+            grid=e(B * P, dt=torch.float32), partial=e(B * ((P + 15) // 16) * EMBED, dt=torch.float32),
             det=e(B, EMBED, dt=torch.float32), score=e(B, dt=torch.float32),
             map=e(B, S, S, dt=torch.float32),
         )
@@ -209,6 +210,13 @@ class VisualEngine:
         for k in chunk_keys[:max(0, len(chunk_keys) - (WS_KEEP - 1))]:
             del self._ws[k]
         self._ws[key] = ws
+        if self.poison:  # test hook: every buffer starts as NaN / 0xFF, so a read-before-write shows
+            for t in list(ws.values()) + ws["taps"]:
+                if isinstance(t, torch.Tensor):
+                    if t.is_floating_point() and t.dtype != FP8:
+                        t.fill_(float("nan"))
+                    else:
+                        t.view(torch.uint8).fill_(0xFF)
         if TUNE and cdt != torch.float32:
             self._tune(ws)
         return ws
@@ -390,8 +398,8 @@ class VisualEngine:
             bounds.append(bounds[-1] + v)
         if len(sizes) == 1:
             seg_raw, det_raw, ws = self.forward_raw(x, slot=_slot0)
-            ops.anomaly_map(seg_raw, T, ws["map"], ws["grid"], g=ws["g"], ksize=k, sigma=s)
-            ops.image_score(det_raw, B, ws["P"], ws["partial"], det=ws["det"], T=T, score=ws["score"])
+            ops.anomaly_map_score(seg_raw, det_raw, T, ws["map"], ws["grid"], ws["partial"], ws["score"],
+                                  g=ws["g"], ksize=k, sigma=s, det=ws["det"])
             return ws["map"], ws["score"]
         key = ("out", B, S, _slot0)
         if key not in self._ws:
@@ -408,23 +416,24 @@ class VisualEngine:
             st.wait_event(ready)
         # every chunk's workspace exists (and, with AACLIP_GEMM_TUNE, is tuned) before any
         # chunk is enqueued: tuning never runs beside the other streams' kernels
-        for i in range(len(sizes)):
-            self._workspace(sizes[i], S, _slot0 + i % nstreams)
+        if os.environ.get("AACLIP_DIAG_NO_PRECREATE") != "1":
+            for i in range(len(sizes)):
+                self._workspace(sizes[i], S, _slot0 + i % nstreams)
         # concurrent chunks share the CUs: one chunk's partial last round of GEMM tiles is
         # filled by the other's work, so the 8-phase 256x256 tile (faster per FLOP) wins
         # even where its tile count rounds up worse than the 320-row tile's (c_fc at 16
         # images per chunk): whole two-stream C2 step 2240 -> 2295 images/s bf16 (2164 ->
         # 2220 fp16); a single stream keeps the heuristic (1895 vs 2050). Thread-local
         # (aaclip_gemm_concurrent), chosen at launch, so graph capture keeps it.
-        with ops.concurrent_gemms(nstreams > 1 and self.dtype in (torch.bfloat16, torch.float16)):
+        with ops.concurrent_gemms(nstreams > 1 and self.dtype in (torch.bfloat16, torch.float16)
+                                  and os.environ.get("AACLIP_DIAG_NO_CONCURRENT") != "1"):
             for i in range(len(sizes)):
                 b0, b1 = bounds[i], bounds[i + 1]
                 st = sts[i % nstreams]
                 with torch.cuda.stream(st):
                     seg_raw, det_raw, ws = self.forward_raw(x[b0:b1], slot=_slot0 + i % nstreams)
-                    ops.anomaly_map(seg_raw, T, out_map[b0:b1], ws["grid"], g=ws["g"], ksize=k, sigma=s)
-                    ops.image_score(det_raw, b1 - b0, ws["P"], ws["partial"], det=ws["det"], T=T,
-                                    score=out_score[b0:b1])
+                    ops.anomaly_map_score(seg_raw, det_raw, T, out_map[b0:b1], ws["grid"], ws["partial"],
+                                          out_score[b0:b1], g=ws["g"], ksize=k, sigma=s, det=ws["det"])
         for st, ev in zip(sts, done):
             ev.record(st)
             main.wait_event(ev)

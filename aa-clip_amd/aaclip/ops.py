@@ -513,11 +513,36 @@ def image_score(det_raw, batch, n_patch, partial, det=None, T=None, score=None, 
     _dev(det_raw, partial, det, T, score)
     _rowmajor(det_raw, "det_raw")
     rows, C = det_raw.shape
-    if rows != batch * n_patch or partial.numel() < batch * ((n_patch + 63) // 64) * C:
+    if rows != batch * n_patch or partial.numel() < batch * ((n_patch + 15) // 16) * C:
         raise ValueError("image_score shape mismatch")
     _launch("image_score", "image_score (det_partial + det_finalize)", 0.0, rows * C * det_raw.element_size(),
             "aaclip_image_score", dtag(det_raw), _ptr(det_raw), det_raw.stride(0), _ptr(T), batch, n_patch, C,
             int(normalize), _ptr(partial), _ptr(det), _ptr(score), _stream())
+
+
+def anomaly_map_score(levels, det_raw, T, out, grid_ws, partial, score, *, g, ksize, sigma, det=None):
+    """The test path's per-batch tail in one pass over the projections (aaclip_anomaly_map_score):
+    the level-summed map of the normalised levels [B*g*g, 768] each, blur + upsample into
+    out [B, S, S], and the image score from det_raw (same row stride as the levels)."""
+    _dev(*levels, det_raw, T, out, grid_ws, partial, score, det)
+    B, S, S2 = out.shape
+    rows, C = levels[0].shape
+    if rows != B * g * g or S != S2 or grid_ws.numel() < rows or grid_ws.dtype != torch.float32:
+        raise ValueError("anomaly_map_score shape mismatch (grid_ws: fp32 >= [B*g*g])")
+    if not out.is_contiguous() or score.numel() < B or partial.numel() < B * ((g * g + 15) // 16) * C:
+        raise ValueError("anomaly_map_score output / workspace too small")
+    for t in list(levels) + [det_raw]:
+        if t.shape != (rows, C) or t.stride(0) != levels[0].stride(0) or t.dtype != levels[0].dtype:
+            raise ValueError("levels and det_raw must share shape, dtype and stride")
+    if det is not None and det.shape != (B, C):
+        raise ValueError("det must be [B, 768]")
+    arr = _level_array(levels)
+    nb = (len(levels) + 1) * rows * C * levels[0].element_size() + C * 2 * 4 + B * S * S * 4 + 2 * rows * 4
+    _launch("anomaly_map", "anomaly_map_score (map_det + blur_upsample + det_finalize)", 0.0, nb,
+            "aaclip_anomaly_map_score", dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(det_raw),
+            _ptr(T), B, g, C, S, ksize, float(sigma), _ptr(grid_ws), _ptr(partial), _ptr(out), _ptr(det),
+            _ptr(score), _stream())
+    return out, score
 
 
 def metrics_eval(pixel_preds: torch.Tensor, pixel_label: torch.Tensor, image_preds: torch.Tensor,

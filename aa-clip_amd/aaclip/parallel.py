@@ -59,7 +59,7 @@ def verify_gather(predict, images_of, s_all: torch.Tensor, s_local: torch.Tensor
     """Self-check of a data-parallel step after the fact, so an N-rank run proves its
     own gathered result: (1) every rank finds its local scores, bit for bit, at its
     shard_range slice of the gathered vector; (2) rank `checker` recomputes the shard of
-    the LAST rank (a foreign shard it never predicted in the step) with
+    the last other rank with images (a foreign shard it never predicted in the step) with
     `predict(images_of(a, b))` and compares it bit for bit with that slice. Per-image
     results do not depend on batch composition (tests/test_e2e_gpu.py), so the foreign
     shard's bits are the same whoever computes them. Both flags are MIN-reduced over
@@ -70,12 +70,36 @@ def verify_gather(predict, images_of, s_all: torch.Tensor, s_local: torch.Tensor
     a, b = shard_range(n_total, rank, world)
     own = bool(torch.equal(s_all[a:b], s_local))
     foreign = True
-    fa, fb = shard_range(n_total, world - 1, world)
+    # the last rank other than the checker with a non-empty shard (the checker's own if none)
+    cand = [r for r in range(world) if r != checker and shard_range(n_total, r, world)[1] > shard_range(n_total, r, world)[0]]
+    who = cand[-1] if cand else checker
+    fa, fb = shard_range(n_total, who, world)
     if rank == checker and fb > fa:
         ref = predict(images_of(fa, fb))
         foreign = bool(torch.equal(s_all[fa:fb], ref.to(s_all.device)))
     flags = torch.tensor([int(own), int(foreign)], dtype=torch.int32, device=s_all.device)
     dist.all_reduce(flags, op=dist.ReduceOp.MIN, group=group)
     return {"backend": str(dist.get_backend(group)), "world": world, "own_slice_verified": bool(flags[0]),
-            "gather_verified": bool(flags[1]), "checked_shard": {"rank": world - 1, "images": [fa, fb],
+            "gather_verified": bool(flags[1]), "checked_shard": {"rank": who, "images": [fa, fb],
                                                                  "checked_by": checker}}
+
+
+def gather_rows_to(local: torch.Tensor, n_total: int, dst: int = 0, group=None):
+    """Gather variable-size row shards (shard_range order) onto rank `dst` only: returns
+    the global [n_total, ...] tensor there and None on the other ranks. For results only
+    one rank consumes (the harness's pixel maps before metrics_eval): 1/world of
+    gather_rows' receive traffic. An empty local shard (n_total < world) still takes
+    part, with zero rows of the right shape."""
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if world == 1:
+        return local
+    rank = dist.get_rank(group)
+    sizes = [shard_range(n_total, r, world) for r in range(world)]
+    width = max(b - a for a, b in sizes)
+    pad = torch.zeros((width,) + tuple(local.shape[1:]), device=local.device, dtype=local.dtype)
+    pad[: local.shape[0]] = local
+    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, gather_list=bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([bufs[r][: b - a] for r, (a, b) in enumerate(sizes)], 0)

@@ -326,21 +326,33 @@ __global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, fl
   }
 }
 
-// Image score, stage 1: per (image, chunk of 64 patches) the sum of
-// normalised det rows -> partial[b][chunk][768]. 4 waves x 16 rows.
-__global__ __launch_bounds__(256) void det_partial_kernel(int in_dtype, const void* det, int64_t ld,
-                                                          int n_patch, int normalize,
-                                                          float* partial, int nchunk) {
+// Image score, stage 1 -- fused with stage 1 of the anomaly map (LEVELS = true): one
+// workgroup per (image, chunk of kDetRows = 16 patches), 4 waves x 4 patch rows in
+// sequence. Per row the wave reads the det_proj row (segbuf's last 768 columns: the
+// same row stride as the levels), normalises it and accumulates it in registers; with
+// LEVELS it also reads that row in every level and writes the level-summed score
+// (patch_row_score, the same bits as patch_scores_kernel) -- one pass over segbuf
+// instead of two. The 4 waves' sums meet in LDS in a fixed order:
+// partial[b][chunk][768] = (w0 + w1) + (w2 + w3). Without LEVELS this is the image
+// score's own stage 1 (aaclip_image_score), with identical det bits.
+constexpr int kDetRows = 16;
+
+template <bool LEVELS, bool F32IN>
+__global__ __launch_bounds__(256) void map_det_kernel(LevelPtrs lv, int nl, int64_t ld, const void* det,
+                                                      const float* T, int n_patch, int normalize, float* grid,
+                                                      float* partial, int nchunk) {
   __shared__ float red[4][768];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int b = blockIdx.y, ch = blockIdx.x;
+  float4_t t0[3], t1[3];
+  if constexpr (LEVELS) load_anchors(T, t0, t1, lane);
   float4_t acc[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-  for (int k = 0; k < 16; ++k) {
-    const int p = ch * 64 + wid * 16 + k;
+  for (int k = 0; k < kDetRows / 4; ++k) {
+    const int p = ch * kDetRows + wid * (kDetRows / 4) + k;
     if (p >= n_patch) break;
     const size_t row = (size_t)b * n_patch + p;
     float4_t v[3];
-    if (in_dtype == AACLIP_F32) {
+    if constexpr (F32IN) {
       const float* q = (const float*)det + row * ld;
 #pragma unroll
       for (int c = 0; c < 3; ++c) v[c] = *(const float4_t*)(q + 256 * c + 4 * lane);
@@ -352,6 +364,10 @@ __global__ __launch_bounds__(256) void det_partial_kernel(int in_dtype, const vo
         v[c] = float4_t{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
                         __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u)};
       }
+    }
+    if constexpr (LEVELS) {
+      const float score = patch_row_score<F32IN>(lv, nl, ld, row, t0, t1, normalize, 0, 1, nullptr, lane);
+      if (lane == 0) grid[row] = score;
     }
     float ss = 0.f;
 #pragma unroll
@@ -507,12 +523,48 @@ extern "C" int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld,
   AACLIP_REQUIRE(det_raw && partial && batch > 0 && n_patch > 0);
   AACLIP_REQUIRE((T && score) || (!T && !score && det));
   AACLIP_REQUIRE(channels == 768 && ld >= channels && ld % 4 == 0);
-  const int nchunk = ceil_div(n_patch, 64);
-  det_partial_kernel<<<dim3(nchunk, batch), 256, 0, (hipStream_t)stream>>>(
-      in_dtype, det_raw, ld, n_patch, normalize, partial, nchunk);
+  const int nchunk = ceil_div(n_patch, kDetRows);
+  const dim3 grd(nchunk, batch);
+  if (in_dtype == AACLIP_F32)
+    map_det_kernel<false, true><<<grd, 256, 0, (hipStream_t)stream>>>(LevelPtrs{}, 0, ld, det_raw, nullptr, n_patch,
+                                                                       normalize, nullptr, partial, nchunk);
+  else
+    map_det_kernel<false, false><<<grd, 256, 0, (hipStream_t)stream>>>(LevelPtrs{}, 0, ld, det_raw, nullptr, n_patch,
+                                                                        normalize, nullptr, partial, nchunk);
   AACLIP_CHECK_LAUNCH();
   det_finalize_kernel<<<batch, 256, 0, (hipStream_t)stream>>>(partial, nchunk, n_patch, T, det,
                                                               score);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_anomaly_map_score(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
+                                        const void* det_raw, const float* T, int batch, int g, int channels,
+                                        int out_size, int ksize, float sigma, float* grid_ws, float* partial,
+                                        float* out, float* det, float* score, void* stream) {
+  AACLIP_REQUIRE(in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16);
+  AACLIP_REQUIRE(levels && det_raw && T && grid_ws && partial && out && score && batch > 0 && g >= 2);
+  AACLIP_REQUIRE(channels == 768 && ld >= channels && ld % 4 == 0);
+  AACLIP_REQUIRE(n_levels >= 1 && n_levels <= kMaxLevels);
+  LevelPtrs lv{};
+  for (int i = 0; i < n_levels; ++i) {
+    AACLIP_REQUIRE(levels[i] != nullptr);
+    lv.p[i] = levels[i];
+  }
+  const int n_patch = g * g;
+  const int nchunk = ceil_div(n_patch, kDetRows);
+  const dim3 grd(nchunk, batch);
+  hipStream_t s = (hipStream_t)stream;
+  if (in_dtype == AACLIP_F32)
+    map_det_kernel<true, true><<<grd, 256, 0, s>>>(lv, n_levels, ld, det_raw, T, n_patch, 1, grid_ws, partial,
+                                                   nchunk);
+  else
+    map_det_kernel<true, false><<<grd, 256, 0, s>>>(lv, n_levels, ld, det_raw, T, n_patch, 1, grid_ws, partial,
+                                                    nchunk);
+  AACLIP_CHECK_LAUNCH();
+  const int rc = aaclip_blur_upsample(grid_ws, out, batch, 1, g, out_size, ksize, sigma, 0, stream);
+  if (rc) return rc;
+  det_finalize_kernel<<<batch, 256, 0, s>>>(partial, nchunk, n_patch, T, det, score);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

@@ -12,10 +12,12 @@ Differences from the reference, all on the host side:
     batch, test.py:85,93); metrics_eval ranks the class's pixels on the device;
   * checkpoints load with torch.load(weights_only=True);
   * --allow_random_init / --dataset synthetic run without the OpenAI weights;
+  * batch k+1 is copied to the device on a copy stream while batch k runs; masks
+    stay on the device until metrics_eval;
   * under torchrun (WORLD_SIZE > 1, one process per GPU) every class's test set is
     sharded by image (aaclip.parallel.shard_range), each rank predicts its shard and
-    the maps / scores / masks / labels are all-gathered (RCCL) before metrics_eval,
-    so every rank computes the same table; rank 0 prints and logs it.
+    the maps / scores / masks / labels are gathered (RCCL) onto rank 0, which runs
+    metrics_eval and prints and logs the table.
 """
 from __future__ import annotations
 
@@ -38,48 +40,86 @@ from utils import setup_seed  # noqa: E402
 
 
 def _device_batch(input_data, prep, device):
-    """Raw uint8 batch (dataset raw=True) -> transformed image / mask tensors on the
-    GPU (aaclip_preprocess_images / aaclip_resize_masks_nearest)."""
-    def run(fn, u8):
-        if isinstance(u8, torch.Tensor):
-            return fn(u8.to(device, non_blocking=True))
-        return torch.cat([fn(t.to(device, non_blocking=True)[None]) for t in u8])
-    return run(prep.images, input_data["image_u8"]), run(prep.masks, input_data["mask_u8"])
+    """One loader batch -> (image fp32 [B,3,S,S], mask uint8 [B,1,S,S]) on the device:
+    raw uint8 batches (dataset raw=True) go through aaclip_preprocess_images /
+    aaclip_resize_masks_nearest, normalised ones are copied (non_blocking from the
+    DataLoader's pinned memory). Runs on the caller's current stream."""
+    if prep is not None:
+        def run(fn, u8):
+            if isinstance(u8, torch.Tensor):
+                return fn(u8.to(device, non_blocking=True))
+            return torch.cat([fn(t.to(device, non_blocking=True)[None]) for t in u8])
+        image, mask = run(prep.images, input_data["image_u8"]), run(prep.masks, input_data["mask_u8"])
+    else:
+        image = input_data["image"].to(device, non_blocking=True)
+        mask = torch.as_tensor(input_data["mask"]).to(device, non_blocking=True)
+    return image, (mask != 0).to(torch.uint8)
 
 
 def get_predictions(model, class_text_embeddings, test_loader, device, img_size, dataset="MVTec", prep=None,
                     n_total=None, streams=1):
-    """test.py:53-99. With n_total (sharded run: test_loader holds this rank's
-    shard_range slice of a class's n_total images) the per-image results of all
-    ranks are all-gathered in shard order, so the return value is the whole class's
-    on every rank. streams: concurrent image chunks per batch (HIP streams) for batches
-    of at least 8 images per chunk; per-image results do not depend on it."""
+    """test.py:53-99. Batch k+1 is copied to the device (and preprocessed, with prep) on a
+    copy stream while batch k runs; maps, scores and masks stay on the device (the
+    reference syncs twice per batch, test.py:85,93). Returns (masks uint8 [N,1,S,S]
+    device tensor, labels numpy [N], maps [N,S,S] and scores [N] device tensors, file
+    names). With n_total (sharded run: test_loader holds this rank's shard_range slice
+    of a class's n_total images) the class is gathered in shard order onto rank 0, which
+    alone runs metrics_eval; the other ranks return None for the tensors. A rank with an
+    empty shard still takes part. streams: concurrent image chunks per batch (HIP
+    streams) for batches of at least 8 images per chunk; results do not depend on it."""
     masks, labels, preds, preds_image, file_names = [], [], [], [], []
-    for input_data in test_loader:
-        if prep is not None:
-            image, mask = _device_batch(input_data, prep, device)
-        else:
-            image, mask = input_data["image"].to(device, non_blocking=True), input_data["mask"]
+    device = torch.device(device)
+    on_gpu = device.type == "cuda"  # (a CPU device only in the host-logic tests, with a stand-in model)
+    main = torch.cuda.current_stream(device) if on_gpu else None
+    copy = torch.cuda.Stream(device=device) if on_gpu else None
+
+    def stage(batch):
+        if not on_gpu:
+            return (batch,) + _device_batch(batch, prep, device) + (None,)
+        with torch.cuda.stream(copy):
+            image, mask = _device_batch(batch, prep, device)
+        ev = torch.cuda.Event()
+        ev.record(copy)
+        return batch, image, mask, ev
+
+    it = iter(test_loader)
+    first = next(it, None)
+    staged = stage(first) if first is not None else None
+    while staged is not None:
+        input_data, image, mask, ready = staged
+        if on_gpu:
+            main.wait_event(ready)
+            image.record_stream(main)
+            mask.record_stream(main)
         class_name = input_data["class_name"]
         assert len(set(class_name)) == 1, "mixed class not supported"
-        masks.append(mask.cpu().numpy())
         labels.append(np.asarray(input_data["label"]))
         file_names.extend(input_data["file_name"])
         nst = streams if image.shape[0] >= 8 * streams else 1
         pmap, score = model.predict(image, class_text_embeddings, DOMAINS[dataset], streams=nst)
         preds.append(pmap.clone())
         preds_image.append(score.clone())
-    # maps and scores stay on the device: metrics_eval ranks them there
-    masks, labels = np.concatenate(masks, axis=0), np.concatenate(labels, axis=0)
-    preds, preds_image = torch.cat(preds), torch.cat(preds_image)
+        masks.append(mask)
+        nxt = next(it, None)  # host: the next batch (loader workers) while this one runs
+        staged = stage(nxt) if nxt is not None else None
+    if preds:
+        masks, labels = torch.cat(masks), np.concatenate(labels, axis=0)
+        preds, preds_image = torch.cat(preds), torch.cat(preds_image)
+    else:  # empty shard (fewer images than ranks): zero rows of the right shapes
+        masks = torch.zeros(0, 1, img_size, img_size, device=device, dtype=torch.uint8)
+        labels = np.zeros(0, dtype=np.int64)
+        preds = torch.zeros(0, img_size, img_size, device=device)
+        preds_image = torch.zeros(0, device=device)
     if n_total is not None:
         import torch.distributed as dist
-        from aaclip.parallel import gather_rows
-        masks = gather_rows(torch.from_numpy(masks).to(preds.device), n_total).cpu().numpy()
-        labels = gather_rows(torch.from_numpy(labels).to(preds.device), n_total).cpu().numpy()
-        preds, preds_image = gather_rows(preds, n_total), gather_rows(preds_image, n_total)
-        names = [None] * dist.get_world_size()
-        dist.all_gather_object(names, file_names)
+        from aaclip.parallel import gather_rows_to
+        lab = gather_rows_to(torch.from_numpy(labels.astype(np.int64)).to(device), n_total)
+        masks, preds, preds_image = (gather_rows_to(t, n_total) for t in (masks, preds, preds_image))
+        names = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
+        dist.gather_object(file_names, names, dst=0)
+        if dist.get_rank() != 0:
+            return None, None, None, None, None
+        labels = lab.cpu().numpy()
         file_names = [f for part in names for f in part]
     return masks, labels, preds, preds_image, file_names
 
@@ -110,8 +150,9 @@ def parse_args(argv=None):
     parser.add_argument("--streams", type=int, default=2,
                         help="concurrent image chunks per batch on HIP streams (bit-identical results; "
                              "batches under 8 images per chunk run as one)")
-    parser.add_argument("--gpu_preprocess", action="store_true",
-                        help="decode on the host, resize + normalise on the GPU (bit-exact with the Pillow path)")
+    parser.add_argument("--gpu_preprocess", action=argparse.BooleanOptionalAction, default=True,
+                        help="real datasets: decode on the host, resize + normalise on the GPU (bit-exact with the "
+                             "Pillow path; the default); --no-gpu_preprocess = the Pillow transform in the workers")
     return parser.parse_args(argv)
 
 
@@ -206,16 +247,20 @@ def run(args):
                     model=model, class_text_embeddings=text_embeddings[class_name], test_loader=loader,
                     device=device, img_size=args.img_size, dataset=args.dataset, prep=prep, n_total=n_total,
                     streams=args.streams)
-            if args.visualize and rank == 0:
-                visualize(masks, preds.cpu().numpy(), file_names, args.save_path, args.dataset, class_name=class_name)
+            if rank != 0:  # the class was gathered onto rank 0, which runs metrics_eval
+                continue
+            if args.visualize:
+                visualize(masks.cpu().numpy(), preds.cpu().numpy(), file_names, args.save_path, args.dataset,
+                          class_name=class_name)
             result = metrics_eval(masks, labels, preds, preds_image, class_name, domain=DOMAINS[args.dataset])
             ctx["classes"][class_name] = (masks, labels, preds, preds_image)
             df.loc[len(df)] = Series(result)
+        if rank != 0:
+            continue
         df.loc[len(df)] = df.drop(columns=["class name"]).mean()
         df.loc[len(df) - 1, "class name"] = "Average"
         logger.info("final results:\n%s", df.to_string(index=False, justify="center"))
-        if rank == 0:
-            print(df.to_string(index=False, justify="center"))
+        print(df.to_string(index=False, justify="center"))
     return df, ctx
 
 

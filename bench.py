@@ -218,27 +218,24 @@ def metrics_leg(dev, size, reps=5):
 
 
 class StepProbe:
-    """HIP timing events around every launch of a captured step (aaclip.ops.set_probe):
-    one external event-record node before and one after each kernel, recorded only
-    while a graph is being captured, so the graph replays the real step with markers
-    in it. elapsed_time(begin, end) after a replay = that launch's GPU duration inside
-    the step (its neighbours, the clock the sustained step holds and, with two
-    streams, the other chunk's concurrent kernels included)."""
+    """HIP timing events around every launch of the step (aaclip.ops.set_probe): an event
+    recorded on the launch's stream right before and right after each kernel, so
+    elapsed_time(begin, end) = that launch's GPU duration inside the running step (its
+    neighbours, the clock the sustained step holds and, with two streams, the other
+    chunk's concurrent kernels included). The step runs EAGERLY here (same kernels,
+    same streams as the timed graph): ROCm's torch refuses event-record nodes inside a
+    captured graph ("External events are disallowed in rocm")."""
 
     def __init__(self):
         self.recs = []
 
     def begin(self, kind, name, flops, nbytes):
-        if not torch.cuda.is_current_stream_capturing():
-            return None
-        e = torch.cuda.Event(enable_timing=True, external=True)
+        e = torch.cuda.Event(enable_timing=True)
         e.record()
         return (kind, name, flops, nbytes, e)
 
     def end(self, tok):
-        if tok is None:
-            return
-        e = torch.cuda.Event(enable_timing=True, external=True)
+        e = torch.cuda.Event(enable_timing=True)
         e.record()
         self.recs.append(tok + (e,))
 
@@ -248,36 +245,36 @@ GEMM_OPS = {"gemm N3072 K1024": "qkv", "gemm N1024 K1024 resid": "out_proj", "ge
             "gemm N1024 K4096 resid": "c_proj", "gemm N1024 K1024 leaky": "adapter"}
 
 
-def in_step_profile(eng, x, T, streams, replays=10):
-    """Capture the C2 step (same engine, batch, domain and stream count as the timed
-    graph) with a StepProbe, replay it `replays` times and average every launch's
-    duration. Returns per-kernel-name and per-op totals per step, the instrumented
-    step time and the sum of launch durations."""
-    B, S = x.shape[0], x.shape[-1]
-    probe = StepProbe()
-    ops.set_probe(probe)
-    try:
-        run = eng.graphed_predict(B, S, "Industrial", streams=streams)
-    finally:
-        ops.set_probe(None)
-    for _ in range(3):
-        run(x, T)
+def in_step_profile(eng, x, T, streams, replays=8):
+    """Run the C2 step (same engine, batch, domain and stream count as the timed graph)
+    eagerly with a StepProbe `replays` times and average every launch's duration.
+    Returns per-kernel-name and per-op totals per step, the probed step's time and the
+    sum of launch durations."""
+    for _ in range(2):
+        eng.predict(x, T, "Industrial", streams=streams)
     torch.cuda.synchronize()
-    n = len(probe.recs)
-    acc = [0.0] * n
     st = torch.cuda.current_stream()
-    t_step = 0.0
+    acc, recs0, t_step = None, None, 0.0
     for _ in range(replays):
+        probe = StepProbe()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        run(x, T)
-        e1.record(st)
+        ops.set_probe(probe)
+        try:
+            e0.record(st)
+            eng.predict(x, T, "Industrial", streams=streams)
+            e1.record(st)
+        finally:
+            ops.set_probe(None)
         e1.synchronize()
+        torch.cuda.synchronize()
         t_step += e0.elapsed_time(e1)
-        for j, r in enumerate(probe.recs):
-            acc[j] += r[4].elapsed_time(r[5])
+        ms = [r[4].elapsed_time(r[5]) for r in probe.recs]
+        if acc is None:
+            acc, recs0 = ms, probe.recs
+        else:
+            acc = [u + v for u, v in zip(acc, ms)]
     by_name, by_op = {}, {}
-    for (kind, name, flops, nbytes, _, _), ms in zip(probe.recs, acc):
+    for (kind, name, flops, nbytes, _, _), ms in zip(recs0, acc):
         ms /= replays
         op = GEMM_OPS.get(kind, kind if not kind.startswith("gemm") else "other_gemm")
         for d, k in ((by_name, name), (by_op, op)):
@@ -294,10 +291,9 @@ def in_step_profile(eng, x, T, streams, replays=10):
             else:
                 e["GBs"] = round(e["bytes"] / (e["ms"] * 1e-3) / 1e9, 1)
             e["ms"] = round(e["ms"], 4)
-    del run
-    torch.cuda.empty_cache()
-    return {"streams": streams, "replays": replays, "launches_per_step": n,
-            "step_ms_instrumented": round(t_step / replays, 3),
+    return {"streams": streams, "replays": replays, "launches_per_step": len(recs0),
+            "method": "eager step, HIP events recorded on each launch's stream right before and after it",
+            "step_ms_probed": round(t_step / replays, 3),
             "sum_of_launch_ms": round(sum(acc) / replays, 3), "by_kernel": by_name, "by_op": by_op}
 
 
@@ -319,9 +315,9 @@ def roofline_from_profiles(p1, p2, B, n_tok):
             "traffic": traffic, "traffic_source": src,
             "avg_launch_us": e["avg_launch_us"], "launches_per_step": e["launches"],
             "flops_per_launch": e["flops"] / e["launches"],
-            "context": (f"in-step: the C2 step (B = {B}, M = {R} rows per GEMM) captured as ONE stream in a "
-                        "hipGraph with HIP event-record nodes around every launch, durations averaged over "
-                        "the replays; the dominant kernel = the GEMM kernel with the most step time"),
+            "context": (f"in-step: the C2 step (B = {B}, M = {R} rows per GEMM) on ONE stream, HIP events "
+                        "recorded right before and after every launch, durations averaged over the probed "
+                        "steps; the dominant kernel = the GEMM kernel with the most step time"),
             "ops_on_this_kernel": [op for op in ops_of if _plan_name(op, R) == dom]}
     blk = [p1["by_op"][k] for k in ("qkv", "attention", "out_proj", "c_fc", "c_proj")]
     bf, bm = sum(v["flops"] for v in blk), sum(v["ms"] for v in blk)
@@ -337,7 +333,7 @@ def roofline_from_profiles(p1, p2, B, n_tok):
         blk2 = [p2["by_op"][k] for k in ("qkv", "attention", "out_proj", "c_fc", "c_proj")]
         bf2, bm2 = sum(v["flops"] for v in blk2), sum(v["ms"] for v in blk2)
         roof["in_step_2stream"] = {
-            "note": "the timed two-stream graph: per-launch durations include the other chunk's concurrent "
+            "note": "the timed two-stream step: per-launch durations include the other chunk's concurrent "
                     "kernels (two launches sharing the CUs each take longer), so these understate each "
                     "kernel's own rate; the throughput of the overlap is in `value`",
             "dominant_kernel_avg_launch_us": e2["avg_launch_us"] if e2 else None,
@@ -355,17 +351,20 @@ def _plan_name(op, R):
 
 
 def map_from_profile(p1, p2):
-    """The anomaly map as one operation (patch_scores + blur_upsample) in the step:
-    algorithmic bytes = L*P*768*4 fp32 level features + anchors read, S*S*4 map
-    written, the P*4 score grid once each way."""
+    """The anomaly map + image score as one operation (aaclip_anomaly_map_score: one pass
+    over the projections, blur + upsample, det finalisation) in the step: algorithmic
+    bytes = (L+1)*P*768*4 fp32 level + det features and the anchors read, S*S*4 map
+    written, the P*4 score grid once each way (plus the det rows the
+    image score needs)."""
     m = p1["by_op"]["anomaly_map"]
     gbs = m["bytes"] / (m["ms"] * 1e-3) / 1e9
     traffic, src = pmc_traffic("map")
-    out = {"kernel": "aaclip_anomaly_map (patch_scores_kernel + blur_upsample_kernel)", "bound": "hbm",
+    out = {"kernel": "aaclip_anomaly_map_score (map_det_kernel + blur_upsample_kernel + det_finalize_kernel)",
+           "bound": "hbm",
            "unit": "GB/s", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
            "traffic": traffic, "traffic_source": src, "avg_launch_us": m["avg_launch_us"],
            "bytes_per_launch": m["bytes"] / m["launches"],
-           "context": "in-step, one stream: the B=32 map after the level projections, HIP events around the op"}
+           "context": "in-step, one stream: the B=32 map + score after the level projections, HIP events around the op"}
     if p2 is not None:
         m2 = p2["by_op"]["anomaly_map"]
         out["in_step_2stream"] = {"avg_launch_us": m2["avg_launch_us"], "GBs": m2["GBs"],
@@ -825,7 +824,15 @@ def main():
     line["tflops_whole_path"] = round(flops_per_image((S // 14) ** 2 + 1) * images / elapsed / 1e12, 1)
     if dist_check is not None:
         line["distributed"] = dist_check
-    if rank == 0 and not args.no_roofline and run is not None:
+    # the timed step's own outputs, checked after the fact: finite, and bit-identical to an
+    # eager one-stream predict of the same images (per-image bits do not depend on chunking)
+    m_t, s_t = last[0].clone(), last[1].clone()
+    m_e, s_e = eng.predict(x, T, "Industrial", streams=1)
+    line["step_outputs_verified"] = {
+        "finite": bool(torch.isfinite(m_t).all() and torch.isfinite(s_t).all()),
+        "equal_to_one_stream_eager": bool(torch.equal(m_t, m_e) and torch.equal(s_t, s_e))}
+    del m_t, s_t
+    if rank == 0 and not args.no_roofline:
         # in-step per-launch durations: the one-stream step (the roofline; a rocprofv3 kernel
         # trace of the same step reproduces it) and the timed two-stream step
         n_tok = (S // 14) ** 2 + 1

@@ -311,12 +311,28 @@ int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n_levels, in
 /*
  * Image-level score: det[b] = mean_p normalize(det_raw[b*n_patch+p]) and
  * score[b] = (det[b] . T[:,1] + 1) / 2. partial: workspace
- * [batch, ceil(n_patch/64), channels] fp32 (fixed-order reduction, deterministic).
+ * [batch, ceil(n_patch/16), channels] fp32 (fixed-order reduction, deterministic).
  * Replaces: model/adapter.py:110-111 + test.py:83-84.
  */
 int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld, const float* T,
                        int batch, int n_patch, int channels, int normalize, float* partial,
                        float* det, float* score, void* stream);
+
+/*
+ * The test path's whole per-batch tail in one pass over the projections: the
+ * level-summed anomaly map (as aaclip_anomaly_map, normalised features) AND the
+ * image score (as aaclip_image_score; same bits for both). Stage 1 reads every
+ * patch row of all n_levels levels and of det_raw (levels[l] and det_raw share the
+ * row stride ld, e.g. the engine's one [rows, (L+1)*768] projection buffer) once,
+ * writing the score grid and the det partials; then blur + upsample and the det
+ * finalisation. grid_ws >= batch*g*g fp32, partial as for aaclip_image_score;
+ * det (optional) [batch, 768], score [batch], out [batch, S, S].
+ * Replaces: test.py:80-93 after the forward + forward_utils.py:196-213.
+ */
+int aaclip_anomaly_map_score(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
+                             const void* det_raw, const float* T, int batch, int g, int channels,
+                             int out_size, int ksize, float sigma, float* grid_ws, float* partial,
+                             float* out, float* det, float* score, void* stream);
 
 /*
  * Device metrics_eval for one class (replaces forward_utils.py:233-280 + the

@@ -87,6 +87,7 @@ def _harness_vs_oracle(tmp_path, dtype, dataset, n, classes, tol_points):
     datasets = get_dataset(dataset, 336, None, -1, "test", synthetic_n=n)
     for cls in classes:
         masks, labels, preds, _ = ctx["classes"][cls]
+        masks = masks.cpu().numpy()  # the harness keeps masks on the device (uint8) until metrics_eval
         imgs = np.stack([datasets[cls][i]["image"].numpy() for i in range(n)])
         T = ctx["text_embeddings"][cls].cpu().numpy()
         ref, ref_maps = _oracle_class_metrics(ctx["model"], T, masks, labels, imgs, dom, cls)

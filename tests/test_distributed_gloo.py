@@ -91,8 +91,8 @@ def _sharded_worker(rank, world, port, n, q):
     pred = lambda xi: model.predict(xi, T)[1]  # noqa: E731
     check = verify_gather(pred, lambda i0, i1: x_global[i0:i1], s_all, s_loc, n)
     bad = s_all.clone()
-    fa, fb = shard_range(n, world - 1, world)
-    bad[fb - 1] += 1.0  # a corrupted gather (last image of the foreign shard) must be caught
+    fa, fb = check["checked_shard"]["images"]
+    bad[fb - 1] += 1.0  # a corrupted gather (last image of the checked shard) must be caught
     check_bad = verify_gather(pred, lambda i0, i1: x_global[i0:i1], bad, s_loc, n)
     # harness: one class's dataset sharded by image, gathered before metrics
     ds = get_dataset("synthetic", 28, None, -1, "test", synthetic_n=n)["bottle"]
@@ -100,17 +100,23 @@ def _sharded_worker(rank, world, port, n, q):
     loader = torch.utils.data.DataLoader(sub, batch_size=3, shuffle=False)
     masks, labels, preds, preds_image, names = harness.get_predictions(model, T, loader, torch.device("cpu"), 28,
                                                                        dataset="synthetic", n_total=n)
-    q.put((rank, s_all.tolist(), m_all.sum().item(), masks.sum(), labels.tolist(), preds.sum().item(),
-           preds_image.tolist(), names, check, check_bad))
+    if rank == 0:  # the class is gathered onto rank 0 (which runs metrics_eval)
+        q.put((rank, s_all.tolist(), m_all.sum().item(), masks.sum().item(), labels.tolist(), preds.sum().item(),
+               preds_image.tolist(), names, check, check_bad))
+    else:
+        assert masks is None and labels is None and preds is None and preds_image is None and names is None
+        q.put((rank, s_all.tolist(), m_all.sum().item(), None, None, None, None, None, check, check_bad))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [8, 7])
+@pytest.mark.parametrize("n", [8, 7, 1])
 def test_gloo_world2_sharded_step_and_harness(n):
     """The bench's data-parallel step (aaclip.parallel.sharded_step) and the harness's
     sharded get_predictions on 2 gloo ranks with a CPU stand-in predictor: every rank
-    ends with exactly the unsharded run's scores, maps, masks, labels and file names."""
+    ends with the unsharded run's gathered scores and maps (the bench step), rank 0 with
+    exactly the unsharded run's class masks, labels, maps, scores and file names (the
+    harness gathers onto rank 0 only), including a rank with an EMPTY shard."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "aa-clip_amd"))
     import test as harness
@@ -137,9 +143,11 @@ def test_gloo_world2_sharded_step_and_harness(n):
     for _, s_all, m_sum, mk_sum, labels, p_sum, pi, names, check, check_bad in out:
         assert check["backend"] == "gloo" and check["world"] == 2
         assert check["gather_verified"] and check["own_slice_verified"], check
-        # the corruption sits in the last rank's own slice and in the foreign shard rank 0 checks
+        # the corruption sits in the checked shard and in its owner's own slice
         assert not check_bad["gather_verified"] and not check_bad["own_slice_verified"], check_bad
         assert s_all == ref_scores.tolist()
         assert m_sum == ref_maps.sum().item()
-        assert mk_sum == ref[0].sum() and labels == ref[1].tolist()
+        if mk_sum is None:
+            continue
+        assert mk_sum == ref[0].sum().item() and labels == ref[1].tolist()
         assert p_sum == ref[2].sum().item() and pi == ref[3].tolist() and names == ref[4]

@@ -227,5 +227,7 @@ def test_concurrent_chunk_pins(dev, weights):
     before = plan()
     m1, s1 = (t.clone() for t in eng.predict(x, T, "Industrial", streams=1))
     m2, s2 = eng.predict(x, T, "Industrial", streams=2)
-    assert torch.equal(m1, m2) and torch.equal(s1, s2)
+    bad = [i for i in range(32) if not torch.equal(m1[i], m2[i])]
+    nan = [i for i in range(32) if torch.isnan(m2[i]).any()]
+    assert not bad and torch.equal(s1, s2), (bad, nan)
     assert plan() == before

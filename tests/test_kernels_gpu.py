@@ -413,7 +413,7 @@ def test_image_score(dev):
     d = rng.standard_normal((B, P, C), dtype=np.float32)
     T = rng.standard_normal((C, 2)).astype(np.float32)
     D = torch.from_numpy(d.reshape(-1, C)).to(dev)
-    partial = torch.empty(B * 9 * C, device=dev)
+    partial = torch.empty(B * 36 * C, device=dev)
     det = torch.empty(B, C, device=dev)
     score = torch.empty(B, device=dev)
     ops.image_score(D, B, P, partial, det=det, T=torch.from_numpy(T).to(dev), score=score)
@@ -526,3 +526,32 @@ def test_similarity_map_train_rejects_too_many_anchors_before_launch(dev):
     f = torch.randn(1, 24 * 24, 768, device=dev)
     with pytest.raises(ValueError):
         calculate_similarity_map(f, torch.randn(768, 9, device=dev), 336, test=False)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,g,S,L,dom", [(3, 24, 336, 4, "Industrial"), (2, 37, 518, 4, "Medical"),
+                                         (2, 32, 448, 6, "Medical"), (1, 5, 70, 1, "Industrial")])
+def test_anomaly_map_score_one_pass(dev, dt, B, g, S, L, dom):
+    """aaclip_anomaly_map_score (one pass over a [rows, (L+1)*768] projection buffer: the
+    engine's segbuf layout, levels then det) = aaclip_anomaly_map + aaclip_image_score bit
+    for bit (map, det and score), P not a multiple of the 16-row det chunk included."""
+    torch.manual_seed(B * g + L)
+    rows = B * g * g
+    buf = torch.randn(rows, (L + 1) * 768, device=dev).to(dt)
+    lv = [buf[:, j * 768:(j + 1) * 768] for j in range(L)]
+    det_raw = buf[:, L * 768:]
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev), dim=0).contiguous()
+    k, sg = (7, 1.0) if dom == "Industrial" else (9, 1.5)
+    grid = torch.empty(rows, device=dev)
+    part = torch.empty(B * ((g * g + 15) // 16) * 768, device=dev)
+    m1, s1, d1 = (torch.empty(B, S, S, device=dev), torch.empty(B, device=dev), torch.empty(B, 768, device=dev))
+    ops.anomaly_map(lv, T, m1, grid, g=g, ksize=k, sigma=sg)
+    ops.image_score(det_raw, B, g * g, part, det=d1, T=T, score=s1)
+    m2, s2, d2 = (torch.full_like(m1, float("nan")), torch.full_like(s1, float("nan")), torch.full_like(d1, float("nan")))
+    grid2 = torch.full_like(grid, float("nan"))
+    ops.anomaly_map_score(lv, det_raw, T, m2, grid2, torch.full_like(part, float("nan")), s2, g=g, ksize=k, sigma=sg,
+                          det=d2)
+    assert torch.equal(m1, m2) and torch.equal(s1, s2) and torch.equal(d1, d2)
+    f = buf.float().view(B, g * g, L + 1, 768)
+    ref_det = torch.nn.functional.normalize(f[:, :, L].double(), dim=-1).mean(1)
+    assert (d2.double() - ref_det).abs().max().item() < 1e-6
