@@ -205,9 +205,14 @@ class VisualEngine:
         def size_of(k):  # (B, S, slot) workspaces, ("out", B, S) chunked-output buffers
             return k[2] if k[0] == "out" else k[1]
 
-        self._ws = {k: v for k, v in self._ws.items() if size_of(k) == S}
-        chunk_keys = [k for k in self._ws if k[0] != "out"]
-        for k in chunk_keys[:max(0, len(chunk_keys) - (WS_KEEP - 1))]:
+        drop = [k for k in self._ws if size_of(k) != S]
+        chunk_keys = [k for k in self._ws if k[0] != "out" and size_of(k) == S]
+        drop += chunk_keys[:max(0, len(chunk_keys) - (WS_KEEP - 1))]
+        if drop and not torch.cuda.is_current_stream_capturing():
+            # a dropped workspace may have been written by another stream than the one it
+            # was allocated on; let that work finish before its memory returns to the pool
+            torch.cuda.synchronize(self.device)
+        for k in drop:
             del self._ws[k]
         self._ws[key] = ws
         if self.poison:  # test hook: every buffer starts as NaN / 0xFF, so a read-before-write shows
@@ -415,9 +420,13 @@ class VisualEngine:
         for st in sts:
             st.wait_event(ready)
         # every chunk's workspace exists (and, with AACLIP_GEMM_TUNE, is tuned) before any
-        # chunk is enqueued: tuning never runs beside the other streams' kernels
-        if os.environ.get("AACLIP_DIAG_NO_PRECREATE") != "1":
-            for i in range(len(sizes)):
+        # chunk is enqueued: tuning never runs beside the other streams' kernels. Each is
+        # allocated on the stream that uses it: the caching allocator orders a block's
+        # reuse only on its allocation stream (allocated on the main stream and written
+        # by a chunk stream, a workspace came back NaN after a long GPU test session:
+        # tests/test_fp16_gpu.py::test_concurrent_chunk_pins in the full suite)
+        for i in range(len(sizes)):
+            with torch.cuda.stream(sts[i % nstreams]):
                 self._workspace(sizes[i], S, _slot0 + i % nstreams)
         # concurrent chunks share the CUs: one chunk's partial last round of GEMM tiles is
         # filled by the other's work, so the 8-phase 256x256 tile (faster per FLOP) wins
@@ -425,8 +434,7 @@ class VisualEngine:
         # images per chunk): whole two-stream C2 step 2240 -> 2295 images/s bf16 (2164 ->
         # 2220 fp16); a single stream keeps the heuristic (1895 vs 2050). Thread-local
         # (aaclip_gemm_concurrent), chosen at launch, so graph capture keeps it.
-        with ops.concurrent_gemms(nstreams > 1 and self.dtype in (torch.bfloat16, torch.float16)
-                                  and os.environ.get("AACLIP_DIAG_NO_CONCURRENT") != "1"):
+        with ops.concurrent_gemms(nstreams > 1 and self.dtype in (torch.bfloat16, torch.float16)):
             for i in range(len(sizes)):
                 b0, b1 = bounds[i], bounds[i + 1]
                 st = sts[i % nstreams]

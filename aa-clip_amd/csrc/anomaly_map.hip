@@ -38,7 +38,7 @@ __device__ __forceinline__ void load_anchors(const float* T, float4_t (&t0)[3], 
 // the two logits [b, 2, group] from lane 0.
 // F32IN: fp32 features (compile time, so every level's loads issue back to back
 // with no per-level dtype branch and its vmcnt(0) join), else bf16.
-template <bool F32IN>
+template <bool F32IN, int NLMAX = kMaxLevels>
 __device__ __forceinline__ float patch_row_score(LevelPtrs lv, int nl, int64_t ld, size_t row,
                                                  const float4_t (&t0)[3], const float4_t (&t1)[3], int normalize,
                                                  int mode, int group, float* out, int lane) {
@@ -46,9 +46,9 @@ __device__ __forceinline__ float patch_row_score(LevelPtrs lv, int nl, int64_t l
   // inlines this (patch_scores_kernel, anomaly_map_kernel), whatever the compiler
   // would fuse in each context
 #pragma clang fp contract(off)
-  float4_t f[kMaxLevels][3];
+  float4_t f[NLMAX][3];
 #pragma unroll
-  for (int l = 0; l < kMaxLevels; ++l) {
+  for (int l = 0; l < NLMAX; ++l) {
     if (l < nl) {
       if constexpr (F32IN) {
         const float* p = (const float*)lv.p[l] + row * ld;
@@ -67,7 +67,7 @@ __device__ __forceinline__ float patch_row_score(LevelPtrs lv, int nl, int64_t l
   }
   float acc = 0.f;
 #pragma unroll
-  for (int l = 0; l < kMaxLevels; ++l) {
+  for (int l = 0; l < NLMAX; ++l) {
     if (l < nl) {
       float ss = 0.f, a0 = 0.f, a1 = 0.f;
 #pragma unroll
@@ -326,86 +326,105 @@ __global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, fl
   }
 }
 
-// Image score, stage 1 -- fused with stage 1 of the anomaly map (LEVELS = true): one
-// workgroup per (image, chunk of kDetRows = 16 patches), 4 waves x 4 patch rows in
-// sequence. Per row the wave reads the det_proj row (segbuf's last 768 columns: the
-// same row stride as the levels), normalises it and accumulates it in registers; with
-// LEVELS it also reads that row in every level and writes the level-summed score
-// (patch_row_score, the same bits as patch_scores_kernel) -- one pass over segbuf
-// instead of two. The 4 waves' sums meet in LDS in a fixed order:
-// partial[b][chunk][768] = (w0 + w1) + (w2 + w3). Without LEVELS this is the image
-// score's own stage 1 (aaclip_image_score), with identical det bits.
+// Image score, stage 1 -- fused with stage 1 of the anomaly map (NL > 0 levels): one
+// workgroup per (image, chunk of kDetRows = 16 patch rows). W = 16 waves take one row
+// each (W = 4: four rows each, in sequence, for NL = 7, 8, whose levels would not fit
+// the 128 registers a 16-wave workgroup allows). Per row the wave reads the det_proj row
+// (segbuf's last 768 columns: the levels' row stride), normalises it into its LDS slot
+// and, with levels, reads that row in every level and writes the level-summed score
+// (patch_row_score: the same bits as patch_scores_kernel) -- one pass over segbuf
+// instead of two. The 16 slots meet in a fixed tree per column, whatever W or NL:
+// partial[b][chunk][j] = ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)) + (same for s8..s15),
+// so the fused pass and aaclip_image_score (NL = 0) give the same det bits.
 constexpr int kDetRows = 16;
 
-template <bool LEVELS, bool F32IN>
-__global__ __launch_bounds__(256) void map_det_kernel(LevelPtrs lv, int nl, int64_t ld, const void* det,
-                                                      const float* T, int n_patch, int normalize, float* grid,
-                                                      float* partial, int nchunk) {
-  __shared__ float red[4][768];
+template <int NL, bool F32IN, int W>
+__global__ __launch_bounds__(64 * W) void map_det_kernel(LevelPtrs lv, int64_t ld, const void* det, const float* T,
+                                                         int n_patch, int normalize, float* grid, float* partial,
+                                                         int nchunk) {
+  static_assert(kDetRows % W == 0, "rows per wave");
+  __shared__ float red[kDetRows][768];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int b = blockIdx.y, ch = blockIdx.x;
   float4_t t0[3], t1[3];
-  if constexpr (LEVELS) load_anchors(T, t0, t1, lane);
-  float4_t acc[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-  for (int k = 0; k < kDetRows / 4; ++k) {
-    const int p = ch * kDetRows + wid * (kDetRows / 4) + k;
-    if (p >= n_patch) break;
-    const size_t row = (size_t)b * n_patch + p;
-    float4_t v[3];
-    if constexpr (F32IN) {
-      const float* q = (const float*)det + row * ld;
+  if constexpr (NL > 0) load_anchors(T, t0, t1, lane);
+#pragma unroll 1
+  for (int k = 0; k < kDetRows / W; ++k) {
+    const int slot = wid * (kDetRows / W) + k;
+    const int p = ch * kDetRows + slot;
+    float4_t v[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    if (p < n_patch) {
+      const size_t row = (size_t)b * n_patch + p;
+      if constexpr (F32IN) {
+        const float* q = (const float*)det + row * ld;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) v[c] = *(const float4_t*)(q + 256 * c + 4 * lane);
-    } else {
-      const uint16_t* q = (const uint16_t*)det + row * ld;
+        for (int c = 0; c < 3; ++c) v[c] = *(const float4_t*)(q + 256 * c + 4 * lane);
+      } else {
+        const uint16_t* q = (const uint16_t*)det + row * ld;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        uint2 r = *(const uint2*)(q + 256 * c + 4 * lane);
-        v[c] = float4_t{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
-                        __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u)};
+        for (int c = 0; c < 3; ++c) {
+          uint2 r = *(const uint2*)(q + 256 * c + 4 * lane);
+          v[c] = float4_t{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
+                          __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u)};
+        }
       }
+      if constexpr (NL > 0) {
+        const float score = patch_row_score<F32IN, NL>(lv, NL, ld, row, t0, t1, normalize, 0, 1, nullptr, lane);
+        if (lane == 0) grid[row] = score;
+      }
+      float ss = 0.f;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ss += v[c][j] * v[c][j];
+      ss = wave_sum(ss);
+      const float inv = normalize ? 1.0f / fmaxf(sqrtf(ss), 1e-12f) : 1.0f;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = v[c] * inv;
     }
-    if constexpr (LEVELS) {
-      const float score = patch_row_score<F32IN>(lv, nl, ld, row, t0, t1, normalize, 0, 1, nullptr, lane);
-      if (lane == 0) grid[row] = score;
-    }
-    float ss = 0.f;
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ss += v[c][j] * v[c][j];
-    ss = wave_sum(ss);
-    const float inv = normalize ? 1.0f / fmaxf(sqrtf(ss), 1e-12f) : 1.0f;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) acc[c] += v[c] * inv;
+    for (int c = 0; c < 3; ++c) *(float4_t*)&red[slot][256 * c + 4 * lane] = v[c];
   }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) *(float4_t*)&red[wid][256 * c + 4 * lane] = acc[c];
   __syncthreads();
-  for (int j = threadIdx.x; j < 768; j += 256) {
-    partial[((size_t)b * nchunk + ch) * 768 + j] = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
+  for (int j = threadIdx.x; j < 768; j += 64 * W) {
+    float h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = red[2 * i][j] + red[2 * i + 1][j];
+    partial[((size_t)b * nchunk + ch) * 768 + j] =
+        ((h[0] + h[1]) + (h[2] + h[3])) + ((h[4] + h[5]) + (h[6] + h[7]));
   }
 }
 
 // Image score, stage 2: det[b] = sum(partials) / n_patch; score = (det.T1 + 1)/2.
-__global__ __launch_bounds__(256) void det_finalize_kernel(const float* partial, int nchunk,
+// One thread per column (768 = 12 waves per image); the partials are summed in chunk
+// order, their loads issued 8 at a time (a chain of 36 dependent loads was latency-bound).
+__global__ __launch_bounds__(768) void det_finalize_kernel(const float* partial, int nchunk,
                                                            int n_patch, const float* T,
                                                            float* det, float* score) {
-  __shared__ float red[4];
-  const int b = blockIdx.x;
-  float dot = 0.f;
-  for (int j = threadIdx.x; j < 768; j += 256) {
-    float s = 0.f;
-    for (int c = 0; c < nchunk; ++c) s += partial[((size_t)b * nchunk + c) * 768 + j];
-    const float m = s / (float)n_patch;
-    if (det) det[(size_t)b * 768 + j] = m;
-    if (T) dot += m * T[2 * j + 1];
+  __shared__ float red[12];
+  const int b = blockIdx.x, j = threadIdx.x;
+  const float* pp = partial + (size_t)b * nchunk * 768 + j;
+  float s = 0.f;
+  for (int c0 = 0; c0 < nchunk; c0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = c0 + i < nchunk ? pp[(size_t)(c0 + i) * 768] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (c0 + i < nchunk) s += v[i];
   }
+  const float m = s / (float)n_patch;
+  if (det) det[(size_t)b * 768 + j] = m;
   if (!score) return;  // block-uniform
-  dot = wave_sum(dot);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dot;
+  float dot = wave_sum(m * T[2 * j + 1]);
+  if ((j & 63) == 0) red[j >> 6] = dot;
   __syncthreads();
-  if (threadIdx.x == 0) score[b] = (((red[0] + red[1]) + (red[2] + red[3])) + 1.0f) / 2.0f;
+  if (j == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 12; i += 4) t += (red[i] + red[i + 1]) + (red[i + 2] + red[i + 3]);
+    score[b] = (t + 1.0f) / 2.0f;
+  }
 }
 
 // kornia 0.6.9 get_gaussian_kernel1d in fp32.
@@ -526,13 +545,13 @@ extern "C" int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld,
   const int nchunk = ceil_div(n_patch, kDetRows);
   const dim3 grd(nchunk, batch);
   if (in_dtype == AACLIP_F32)
-    map_det_kernel<false, true><<<grd, 256, 0, (hipStream_t)stream>>>(LevelPtrs{}, 0, ld, det_raw, nullptr, n_patch,
+    map_det_kernel<0, true, 16><<<grd, 1024, 0, (hipStream_t)stream>>>(LevelPtrs{}, ld, det_raw, nullptr, n_patch,
                                                                        normalize, nullptr, partial, nchunk);
   else
-    map_det_kernel<false, false><<<grd, 256, 0, (hipStream_t)stream>>>(LevelPtrs{}, 0, ld, det_raw, nullptr, n_patch,
+    map_det_kernel<0, false, 16><<<grd, 1024, 0, (hipStream_t)stream>>>(LevelPtrs{}, ld, det_raw, nullptr, n_patch,
                                                                         normalize, nullptr, partial, nchunk);
   AACLIP_CHECK_LAUNCH();
-  det_finalize_kernel<<<batch, 256, 0, (hipStream_t)stream>>>(partial, nchunk, n_patch, T, det,
+  det_finalize_kernel<<<batch, 768, 0, (hipStream_t)stream>>>(partial, nchunk, n_patch, T, det,
                                                               score);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
@@ -555,16 +574,25 @@ extern "C" int aaclip_anomaly_map_score(int in_dtype, const void* const* levels,
   const int nchunk = ceil_div(n_patch, kDetRows);
   const dim3 grd(nchunk, batch);
   hipStream_t s = (hipStream_t)stream;
-  if (in_dtype == AACLIP_F32)
-    map_det_kernel<true, true><<<grd, 256, 0, s>>>(lv, n_levels, ld, det_raw, T, n_patch, 1, grid_ws, partial,
-                                                   nchunk);
-  else
-    map_det_kernel<true, false><<<grd, 256, 0, s>>>(lv, n_levels, ld, det_raw, T, n_patch, 1, grid_ws, partial,
-                                                    nchunk);
+  const bool f32 = in_dtype == AACLIP_F32;
+#define MD_LAUNCH(NL, W)                                                                                         \
+  (f32 ? map_det_kernel<NL, true, W><<<grd, 64 * W, 0, s>>>(lv, ld, det_raw, T, n_patch, 1, grid_ws, partial, nchunk) \
+       : map_det_kernel<NL, false, W><<<grd, 64 * W, 0, s>>>(lv, ld, det_raw, T, n_patch, 1, grid_ws, partial, nchunk))
+  switch (n_levels) {  // 16 one-row waves while NL levels fit 128 registers (NL <= 6), else 4 waves x 4 rows
+    case 1: MD_LAUNCH(1, 16); break;
+    case 2: MD_LAUNCH(2, 16); break;
+    case 3: MD_LAUNCH(3, 16); break;
+    case 4: MD_LAUNCH(4, 16); break;
+    case 5: MD_LAUNCH(5, 16); break;
+    case 6: MD_LAUNCH(6, 16); break;
+    case 7: MD_LAUNCH(7, 4); break;
+    default: MD_LAUNCH(8, 4); break;
+  }
+#undef MD_LAUNCH
   AACLIP_CHECK_LAUNCH();
   const int rc = aaclip_blur_upsample(grid_ws, out, batch, 1, g, out_size, ksize, sigma, 0, stream);
   if (rc) return rc;
-  det_finalize_kernel<<<batch, 256, 0, s>>>(partial, nchunk, n_patch, T, det, score);
+  det_finalize_kernel<<<batch, 768, 0, s>>>(partial, nchunk, n_patch, T, det, score);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

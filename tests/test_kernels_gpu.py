@@ -530,7 +530,8 @@ def test_similarity_map_train_rejects_too_many_anchors_before_launch(dev):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,g,S,L,dom", [(3, 24, 336, 4, "Industrial"), (2, 37, 518, 4, "Medical"),
-                                         (2, 32, 448, 6, "Medical"), (1, 5, 70, 1, "Industrial")])
+                                         (2, 32, 448, 6, "Medical"), (1, 5, 70, 1, "Industrial"),
+                                         (2, 8, 112, 7, "Industrial"), (1, 9, 120, 8, "Medical")])
 def test_anomaly_map_score_one_pass(dev, dt, B, g, S, L, dom):
     """aaclip_anomaly_map_score (one pass over a [rows, (L+1)*768] projection buffer: the
     engine's segbuf layout, levels then det) = aaclip_anomaly_map + aaclip_image_score bit
