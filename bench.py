@@ -351,20 +351,17 @@ def _plan_name(op, R):
 
 
 def map_from_profile(p1, p2):
-    """The anomaly map + image score as one operation (aaclip_anomaly_map_score: one pass
-    over the projections, blur + upsample, det finalisation) in the step: algorithmic
-    bytes = (L+1)*P*768*4 fp32 level + det features and the anchors read, S*S*4 map
-    written, the P*4 score grid once each way (plus the det rows the
-    image score needs)."""
+    """The anomaly map as one operation (aaclip_anomaly_map: patch_scores + blur_upsample)
+    in the step: algorithmic bytes = L*P*768*4 fp32 level features + anchors read, S*S*4
+    map written, the P*4 score grid once each way."""
     m = p1["by_op"]["anomaly_map"]
     gbs = m["bytes"] / (m["ms"] * 1e-3) / 1e9
     traffic, src = pmc_traffic("map")
-    out = {"kernel": "aaclip_anomaly_map_score (map_det_kernel + blur_upsample_kernel + det_finalize_kernel)",
-           "bound": "hbm",
+    out = {"kernel": "aaclip_anomaly_map (patch_scores_kernel + blur_upsample_kernel)", "bound": "hbm",
            "unit": "GB/s", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
            "traffic": traffic, "traffic_source": src, "avg_launch_us": m["avg_launch_us"],
            "bytes_per_launch": m["bytes"] / m["launches"],
-           "context": "in-step, one stream: the B=32 map + score after the level projections, HIP events around the op"}
+           "context": "in-step, one stream: the B=32 map after the level projections, HIP events around the op"}
     if p2 is not None:
         m2 = p2["by_op"]["anomaly_map"]
         out["in_step_2stream"] = {"avg_launch_us": m2["avg_launch_us"], "GBs": m2["GBs"],

@@ -247,3 +247,20 @@ def test_518_default_size_parity(dev, dtype):
         assert flips == 0
     if dtype == torch.float32:
         np.testing.assert_allclose(grid, ref, atol=5e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_text_encode_truncation_is_exact(dev, golden, weights, dtype):
+    """TextEngine.encode drops the token columns after the longest prompt's EOT (the tower
+    is causal): bit-identical to running all 77 columns, adapted and unadapted, for one
+    class's prompts and for a mixed-length batch."""
+    sd, _, ta, _ = weights
+    tp = {k: v for k, v in sd.items() if not k.startswith("visual.")}
+    t = golden["text"]
+    tok = torch.cat([torch.from_numpy(t["bottle_tok_abnormal"]), torch.from_numpy(t["brain_tok_normal"])]).to(dev)
+    for ad in (ta, None):
+        eng = TextEngine(tp, ad, dtype=dtype)
+        full = eng.encode(tok, truncate=False).clone()
+        assert int(tok.argmax(-1).max()) + 1 < tok.shape[1]  # the case actually truncates
+        assert torch.equal(eng.encode(tok), full)
+        assert torch.equal(eng.encode(tok[:3]), full[:3])

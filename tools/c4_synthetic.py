@@ -49,29 +49,32 @@ def build(dev, dtype):
     return m
 
 
-def class_batches(ds, n, bs):
+def class_batches(ds, n, bs, pin=False):
+    """The DataLoader's batches of one class (dicts as test.py's loop reads them), pinned
+    host memory like DataLoader(pin_memory=True)."""
+    out = []
     for b0 in range(0, n, bs):
         items = [ds[i] for i in range(b0, min(n, b0 + bs))]
-        yield (torch.stack([it["image"] for it in items]), np.stack([it["mask"].numpy() for it in items]),
-               np.array([it["label"] for it in items]))
+        img = torch.stack([it["image"] for it in items])
+        msk = torch.stack([it["mask"] for it in items])
+        out.append({"image": img.pin_memory() if pin else img, "mask": msk.pin_memory() if pin else msk,
+                    "label": torch.tensor([it["label"] for it in items]),
+                    "class_name": [it["class_name"] for it in items], "file_name": [it["file_name"] for it in items]})
+    return out
 
 
-def gpu_eval(model, datasets, n, bs, dev, pinned):
-    """test.py:185-236 for every class; returns per-class metrics, maps, scores."""
+def gpu_eval(model, datasets, dev, batches):
+    """test.py:185-236 for every class through the harness's own get_predictions (copy
+    stream prefetch of batch k+1 under batch k, maps / masks kept on the device) and
+    the device metrics_eval; returns per-class metrics, maps, scores."""
+    import test as harness
     dom = DOMAINS[DS]
     out = {}
     with torch.no_grad():
         T = get_adapted_text_embedding(model, DS, dev)
-        for c, ds in datasets.items():
-            masks, labels, preds, scores = [], [], [], []
-            for img, msk, lab in pinned[c] if pinned else class_batches(ds, n, bs):
-                pmap, s = model.predict(img.to(dev, non_blocking=True), T[c], dom, streams=2)
-                preds.append(pmap.clone())
-                scores.append(s.clone())
-                masks.append(msk)
-                labels.append(lab)
-            masks, labels = np.concatenate(masks), np.concatenate(labels)
-            preds, scores = torch.cat(preds), torch.cat(scores)
+        for c in datasets:
+            masks, labels, preds, scores, _ = harness.get_predictions(model, T[c], batches[c], dev, 336,
+                                                                      dataset=DS, streams=2)
             out[c] = (metrics_eval(masks, labels, preds, scores, c, domain=dom), preds, scores, masks, labels)
     return T, out
 
@@ -86,16 +89,15 @@ def main():
     dev = torch.device("cuda:0")
     datasets = get_dataset(DS, 336, None, -1, "test", synthetic_n=a.n)
     # host-side batches prepared once (pinned), as the DataLoader workers would
-    pinned = {c: [(img.pin_memory(), m, lab) for img, m, lab in class_batches(ds, a.n, a.bs)]
-              for c, ds in datasets.items()}
+    pinned = {c: class_batches(ds, a.n, a.bs, pin=True) for c, ds in datasets.items()}
     res = {"workload": f"C4-synthetic: 15 MVTec classes x {a.n} synthetic 336px images, ensemble prompts "
                        f"(adapted text tower), batch {a.bs}, 4 levels, metrics_eval per class, 1 GPU",
            "data": "synthetic weights (oracle/synth.py) and seeded synthetic images/masks (dataset synthetic_mvtec)"}
     model = build(dev, torch.bfloat16)
-    gpu_eval(model, datasets, a.n, a.bs, dev, pinned)  # warm-up: engines, workspaces, graphs
+    gpu_eval(model, datasets, dev, pinned)  # warm-up: engines, workspaces, graphs
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    _, out16 = gpu_eval(model, datasets, a.n, a.bs, dev, pinned)
+    _, out16 = gpu_eval(model, datasets, dev, pinned)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     n_img = a.n * len(datasets)
@@ -118,17 +120,18 @@ def main():
         for c, ds in datasets.items():
             sn, sa = _sentences(REAL_NAMES[DS][c])
             Tc = R.class_anchor(sd, ta, tokenize(sn).numpy(), tokenize(sa).numpy())
-            img, msk, lab = next(class_batches(ds, a.cpu_n, a.cpu_n))
-            seg, det = R.visual_forward(sd, ia, img.numpy())
+            bt = class_batches(ds, a.cpu_n, a.cpu_n)[0]
+            seg, det = R.visual_forward(sd, ia, bt["image"].numpy())
             maps = R.anomaly_map(seg, Tc, 336, DOMAINS[DS])
             sc = R.image_score(det, Tc)
-            ref[c] = (Tc, R.metrics_eval(msk[:, 0], lab, maps, sc, c, DOMAINS[DS]), maps, sc)
+            ref[c] = (Tc, R.metrics_eval(bt["mask"].numpy()[:, 0], bt["label"].numpy(), maps, sc, c, DOMAINS[DS]),
+                      maps, sc)
             print(f"cpu reference: class {c} done ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
         cpu_dt = time.perf_counter() - t0
         for tag, dt_ in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
             model = build(dev, dt_)
-            sub = {c: [tuple(next(class_batches(ds, a.cpu_n, a.cpu_n)))] for c, ds in datasets.items()}
-            T, out = gpu_eval(model, datasets, a.cpu_n, a.cpu_n, dev, sub)
+            sub = {c: class_batches(ds, a.cpu_n, a.cpu_n) for c, ds in datasets.items()}
+            T, out = gpu_eval(model, datasets, dev, sub)
             rows = {}
             for c in datasets:
                 g, r = out[c][0], ref[c][1]
