@@ -455,6 +455,28 @@ class VisualEngine:
             main.wait_event(ev)
         return out_map, out_score
 
+    GRAPH_CACHE = 4  # captured steps kept per engine (predict_cached)
+
+    def predict_cached(self, x: torch.Tensor, T: torch.Tensor, domain: str = "Industrial", streams=1):
+        """predict() through a captured hipGraph once a (batch, size, domain, streams) shape
+        repeats (the harness's full batches): the first call of a shape runs eagerly, the
+        second captures, later ones replay (inputs copied into the graph's static
+        buffers). Same kernels, same bits (tests/test_e2e_gpu.py); the outputs are
+        graph-owned buffers, overwritten by the next replay of that shape."""
+        key = (x.shape[0], x.shape[-1], domain, tuple(streams) if isinstance(streams, (tuple, list)) else streams)
+        if not hasattr(self, "_graph_cache"):
+            self._graph_cache, self._seen = {}, {}
+        run = self._graph_cache.get(key)
+        if run is None:
+            self._seen[key] = self._seen.get(key, 0) + 1
+            if self._seen[key] < 2 or not x.is_cuda:
+                return self.predict(x, T, domain, streams=streams)
+            if len(self._graph_cache) >= self.GRAPH_CACHE:
+                self._graph_cache.pop(next(iter(self._graph_cache)))
+            run = self.graphed_predict(x.shape[0], x.shape[-1], domain, streams=streams)
+            self._graph_cache[key] = run
+        return run(x, T.to(self.device, torch.float32))
+
     @torch.no_grad()
     @_on_device
     def graphed_predict(self, batch: int, img_size: int, domain: str = "Industrial", streams: int = 1):

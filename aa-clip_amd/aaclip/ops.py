@@ -562,7 +562,23 @@ def metrics_eval(pixel_preds: torch.Tensor, pixel_label: torch.Tensor, image_pre
     if ip.numel() != N or il.numel() != N:
         raise ValueError("image_preds / image_label must have one entry per image")
     with torch.cuda.device(preds.device):
-        return _metrics_eval_dev(preds, lab, ip, il, N, pix, medical)
+        return _metrics_eval_dev(preds, lab, ip, il, N, pix, medical).tolist()
+
+
+def metrics_eval_device(pixel_preds, pixel_label, image_preds, image_label, *, medical: bool) -> torch.Tensor:
+    """metrics_eval without the host sync: the device float64[4] result, read later (the
+    harness reads every class's at the end, so classes are enqueued back to back)."""
+    N = pixel_preds.shape[0]
+    preds = pixel_preds.reshape(N, -1).to(torch.float32).contiguous()
+    lab = (pixel_label.reshape(N, -1) != 0).to(torch.uint8).contiguous()
+    if lab.shape[1] != preds.shape[1]:
+        raise ValueError("pixel_label and pixel_preds must have the same number of elements per image")
+    ip = image_preds.reshape(-1).to(torch.float32).contiguous()
+    il = (image_label.reshape(-1) != 0).to(torch.uint8).contiguous()
+    if ip.numel() != N or il.numel() != N:
+        raise ValueError("image_preds / image_label must have one entry per image")
+    with torch.cuda.device(preds.device):
+        return _metrics_eval_dev(preds, lab, ip, il, N, preds.shape[1], medical)
 
 
 def _metrics_eval_dev(preds, lab, ip, il, N, pix, medical):
@@ -574,4 +590,4 @@ def _metrics_eval_dev(preds, lab, ip, il, N, pix, medical):
     out = torch.empty(4, device=preds.device, dtype=torch.float64)
     call("aaclip_metrics_eval", _ptr(preds), _ptr(lab), _ptr(ip), _ptr(il), N, pix, int(medical),
          ws.data_ptr() + off, need.value, _ptr(out), _stream())
-    return out.tolist()
+    return out

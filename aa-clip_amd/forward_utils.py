@@ -129,6 +129,13 @@ def metrics_eval(pixel_label, image_label, pixel_preds, image_preds, class_names
     """forward_utils.py:233-280 on the device (aaclip_metrics_eval: class min-max, score
     fusion, exact tie-aware AUROC / AP). Tensors or numpy arrays; the rounding and the
     dict layout are the reference's. There is no CPU path: without a GPU this raises."""
+    return metrics_eval_deferred(pixel_label, image_label, pixel_preds, image_preds, class_names, domain)()
+
+
+def metrics_eval_deferred(pixel_label, image_label, pixel_preds, image_preds, class_names: str, domain: str):
+    """metrics_eval enqueued on the device now, read later: returns a function that syncs
+    and builds the reference's dict. The harness enqueues every class before reading any,
+    so no class waits for the previous one's metrics on the host."""
     if not torch.cuda.is_available():
         raise RuntimeError("metrics_eval runs on the MI355X kernels (aaclip_metrics_eval); no GPU is visible "
                            "and there is no CPU path")
@@ -137,11 +144,15 @@ def metrics_eval(pixel_label, image_label, pixel_preds, image_preds, class_names
     t = [x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x))
          for x in (pixel_preds, pixel_label, image_preds, image_label)]
     t = [x.to(dev, non_blocking=True) for x in t]
-    pauc, pap, iauc, iap = ops.metrics_eval(t[0], t[1], t[2], t[3], medical=(domain == "Medical"))
-    if pauc != pauc:  # NaN: one pixel class only, sklearn raises here
-        raise ValueError("Only one class present in y_true. ROC AUC score is not defined in that case.")
-    return {"class name": class_names, "pixel AUC": round(pauc, 4) * 100, "pixel AP": round(pap, 4) * 100,
-            "image AUC": round(iauc, 4) * 100, "image AP": round(iap, 4) * 100}
+    res = ops.metrics_eval_device(t[0], t[1], t[2], t[3], medical=(domain == "Medical"))
+
+    def read():
+        pauc, pap, iauc, iap = res.tolist()
+        if pauc != pauc:  # NaN: one pixel class only, sklearn raises here
+            raise ValueError("Only one class present in y_true. ROC AUC score is not defined in that case.")
+        return {"class name": class_names, "pixel AUC": round(pauc, 4) * 100, "pixel AP": round(pap, 4) * 100,
+                "image AUC": round(iauc, 4) * 100, "image AP": round(iap, 4) * 100}
+    return read
 
 
 def visualize(pixel_label, pixel_preds, file_names, save_dir, dataset_name, class_name):

@@ -103,8 +103,10 @@ class AdaptedCLIP(nn.Module):
     def predict(self, x, text_features, domain="Industrial", streams=1):
         """Fused test path (test.py:80-93): (anomaly map [B,S,S], image score [B]), fp32.
         streams > 1 (or a tuple of chunk sizes) runs image chunks on that many HIP
-        streams (VisualEngine.predict); per-image results do not depend on it."""
-        return self.visual_engine().predict(x, text_features, domain, streams=streams)
+        streams (VisualEngine.predict); per-image results do not depend on it. A shape seen
+        before replays a captured hipGraph of the step (VisualEngine.predict_cached).
+        The outputs are engine-owned buffers: clone them to keep them (test.py does)."""
+        return self.visual_engine().predict_cached(x, text_features, domain, streams=streams)
 
     def encode_text(self, text, adapt_text=True):
         if not adapt_text:

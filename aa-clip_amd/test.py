@@ -33,7 +33,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from dataset import DOMAINS, get_dataset  # noqa: E402
-from forward_utils import get_adapted_text_embedding, metrics_eval, visualize  # noqa: E402
+from forward_utils import get_adapted_text_embedding, metrics_eval_deferred, visualize  # noqa: E402
 from model.adapter import AdaptedCLIP  # noqa: E402
 from model.clip import create_model  # noqa: E402
 from utils import setup_seed  # noqa: E402
@@ -229,6 +229,7 @@ def run(args):
         with torch.no_grad():
             text_embeddings = get_adapted_text_embedding(model if adapt_text else clip_model, args.dataset, device)
         df = DataFrame(columns=["class name", "pixel AUC", "pixel AP", "image AUC", "image AP"])
+        pending = []
         ctx = {"model": model, "text_embeddings": text_embeddings, "classes": {}}
         for class_name, image_dataset in image_datasets.items():
             workers = 0 if synthetic else 4
@@ -252,9 +253,12 @@ def run(args):
             if args.visualize:
                 visualize(masks.cpu().numpy(), preds.cpu().numpy(), file_names, args.save_path, args.dataset,
                           class_name=class_name)
-            result = metrics_eval(masks, labels, preds, preds_image, class_name, domain=DOMAINS[args.dataset])
+            # enqueued now, read after the loop: the next class's batches start at once
+            pending.append(metrics_eval_deferred(masks, labels, preds, preds_image, class_name,
+                                                 domain=DOMAINS[args.dataset]))
             ctx["classes"][class_name] = (masks, labels, preds, preds_image)
-            df.loc[len(df)] = Series(result)
+        for read in pending:
+            df.loc[len(df)] = Series(read())
         if rank != 0:
             continue
         df.loc[len(df)] = df.drop(columns=["class name"]).mean()

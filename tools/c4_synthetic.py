@@ -28,7 +28,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "aa-clip_amd")]
 from dataset import DOMAINS, get_dataset  # noqa: E402
-from forward_utils import _sentences, get_adapted_text_embedding, metrics_eval  # noqa: E402
+from forward_utils import _sentences, get_adapted_text_embedding, metrics_eval, metrics_eval_deferred  # noqa: E402,E501
 from model.adapter import AdaptedCLIP  # noqa: E402
 from model.clip import create_model  # noqa: E402
 from model.tokenizer import tokenize  # noqa: E402
@@ -75,8 +75,9 @@ def gpu_eval(model, datasets, dev, batches):
         for c in datasets:
             masks, labels, preds, scores, _ = harness.get_predictions(model, T[c], batches[c], dev, 336,
                                                                       dataset=DS, streams=2)
-            out[c] = (metrics_eval(masks, labels, preds, scores, c, domain=dom), preds, scores, masks, labels)
-    return T, out
+            out[c] = (metrics_eval_deferred(masks, labels, preds, scores, c, domain=dom), preds, scores, masks,
+                      labels)
+    return T, {c: (v[0](),) + v[1:] for c, v in out.items()}  # read every class's metrics after the last
 
 
 def main():
@@ -104,6 +105,34 @@ def main():
     res["bf16_whole_eval"] = {"seconds": round(dt, 4), "images": n_img, "images_per_sec": round(n_img / dt, 1),
                               "includes": "H2D copies of the pinned batches, 15 text anchors (240 prompts), "
                                           "forward + map + score, per-class device metrics"}
+    # where the whole-eval time goes (each phase alone, synchronised; not the timed flow)
+    import test as harness
+
+    def timed(fn, reps=3):
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / reps
+
+    with torch.no_grad():
+        Tall = get_adapted_text_embedding(model, DS, dev)
+        c0 = next(iter(datasets))
+        x0 = pinned[c0][0]["image"].to(dev)
+        res["breakdown_seconds"] = {
+            "text_anchors_240_prompts": round(timed(lambda: get_adapted_text_embedding(model, DS, dev)), 4),
+            "predict_b32_eager_x15": round(15 * timed(lambda: model.predict(x0, Tall[c0], DOMAINS[DS], streams=2)), 4),
+            "get_predictions_x15": round(15 * timed(lambda: harness.get_predictions(
+                model, Tall[c0], pinned[c0], dev, 336, dataset=DS, streams=2)), 4),
+            "metrics_eval_x15": round(15 * timed(lambda: metrics_eval(out16[c0][3], out16[c0][4], out16[c0][1],
+                                                                        out16[c0][2], c0, domain=DOMAINS[DS])), 4)}
+        eng = model.visual_engine()
+        run = eng.graphed_predict(x0.shape[0], 336, DOMAINS[DS], streams=2)
+        res["breakdown_seconds"]["predict_b32_graph_x15"] = round(15 * timed(lambda: run(x0, Tall[c0])), 4)
+        del run
+    print(json.dumps(res["breakdown_seconds"]), flush=True)
     mean = {k: float(np.mean([out16[c][0][k] for c in out16])) for k in ("pixel AUC", "pixel AP", "image AUC",
                                                                         "image AP")}
     res["bf16_mean_metrics"] = mean
