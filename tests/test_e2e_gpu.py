@@ -264,3 +264,19 @@ def test_text_encode_truncation_is_exact(dev, golden, weights, dtype):
         assert int(tok.argmax(-1).max()) + 1 < tok.shape[1]  # the case actually truncates
         assert torch.equal(eng.encode(tok), full)
         assert torch.equal(eng.encode(tok[:3]), full[:3])
+
+
+def test_predict_cached_replays_graph_bit_identical(dev, weights):
+    """VisualEngine.predict_cached (AdaptedCLIP.predict): eager on a shape's first call,
+    captured on the second, replayed after -- every call bit-identical to predict(),
+    with new images and anchors each time, two shapes interleaved."""
+    eng = _visual(weights, torch.bfloat16)
+    g = torch.Generator(device=dev).manual_seed(21)
+    for rep in range(4):
+        for B, streams in ((4, 2), (2, 1)):
+            x = torch.randn(B, 3, 336, 336, device=dev, generator=g)
+            T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
+            m1, s1 = (t.clone() for t in eng.predict_cached(x, T, "Industrial", streams=streams))
+            m0, s0 = eng.predict(x, T, "Industrial", streams=streams)
+            assert torch.equal(m1, m0) and torch.equal(s1, s0), (rep, B)
+    assert len(eng._graph_cache) == 2

@@ -34,6 +34,7 @@ from model.clip import create_model  # noqa: E402
 from model.tokenizer import tokenize  # noqa: E402
 from dataset.constants import REAL_NAMES  # noqa: E402
 from oracle import aaclip_np as R  # noqa: E402
+from oracle import aaclip_torch as RT  # noqa: E402
 from oracle import synth  # noqa: E402
 
 DS = "synthetic_mvtec"
@@ -143,6 +144,8 @@ def main():
     if a.cpu_n > 0:
         sd = synth.clip_state_dict(111)
         ia, ta = synth.adapter_state_dicts(111)
+        tw = RT.prepare(sd, ia)
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
         par = {}
         t0 = time.perf_counter()
         ref = {}
@@ -150,9 +153,11 @@ def main():
             sn, sa = _sentences(REAL_NAMES[DS][c])
             Tc = R.class_anchor(sd, ta, tokenize(sn).numpy(), tokenize(sa).numpy())
             bt = class_batches(ds, a.cpu_n, a.cpu_n)[0]
-            seg, det = R.visual_forward(sd, ia, bt["image"].numpy())
-            maps = R.anomaly_map(seg, Tc, 336, DOMAINS[DS])
-            sc = R.image_score(det, Tc)
+            with torch.no_grad():  # the torch-CPU oracle (same arithmetic as the numpy one, ATen speed)
+                seg, det = RT.visual_forward(tw, bt["image"])
+                Tt = torch.from_numpy(Tc)
+                maps = RT.anomaly_map(seg, Tt, 336, DOMAINS[DS]).numpy()
+                sc = RT.image_score(det, Tt).numpy()
             ref[c] = (Tc, R.metrics_eval(bt["mask"].numpy()[:, 0], bt["label"].numpy(), maps, sc, c, DOMAINS[DS]),
                       maps, sc)
             print(f"cpu reference: class {c} done ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
@@ -178,7 +183,8 @@ def main():
                         "per_class": rows}
             del model
             torch.cuda.empty_cache()
-        res["parity"] = {"images_per_class": a.cpu_n, "reference": "numpy oracle + sklearn (CPU), same weights/inputs",
+        res["parity"] = {"images_per_class": a.cpu_n, "reference": "CPU oracle (text anchors: numpy oracle; visual "
+                                                                  "path: torch-CPU oracle) + sklearn, same weights/inputs",
                          "image_metrics_degenerate": a.cpu_n < 8,
                          "cpu_seconds": round(cpu_dt, 1), **par}
     line = json.dumps(res)
