@@ -1,0 +1,18 @@
+# GPU box: full GPU test suite, smoke(), the default bench line, C4-synthetic with its
+# parity subset; stops after any fault / abort / timeout. usage: bash tools/gpu_final.sh TAG
+set -o pipefail
+TAG=${1:-final}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 --timeout-method thread \
+  > $OUT/pytest.log 2>&1
+rc=$?
+tail -3 $OUT/pytest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; exit 3; }
+tail -1 $OUT/smoke.log
+timeout -k 10 900 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -5 $OUT/bench.err; exit 4; }
+timeout -k 10 600 python -u tools/c4_synthetic.py --cpu-n 8 --out $OUT/c4.json > $OUT/c4.log 2>&1 || { echo c4 failed; exit 5; }
+exit $rc
