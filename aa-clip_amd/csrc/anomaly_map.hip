@@ -96,7 +96,10 @@ __device__ __forceinline__ float patch_row_score(LevelPtrs lv, int nl, int64_t l
   return acc;
 }
 
-template <bool F32IN>
+// NLMAX: registers for that many levels (the level count at compile time where it is
+// known: 4 levels of fp32 rows take 48 registers instead of kMaxLevels' 96, which
+// lets 5 instead of 4 waves per SIMD keep their loads in flight).
+template <bool F32IN, int NLMAX = kMaxLevels>
 __global__ __launch_bounds__(256) void patch_scores_kernel(LevelPtrs lv, int nl,
                                                            int64_t ld, const float* T, int rows,
                                                            int normalize, int mode, int group,
@@ -106,7 +109,8 @@ __global__ __launch_bounds__(256) void patch_scores_kernel(LevelPtrs lv, int nl,
   if (row >= rows) return;
   float4_t t0[3], t1[3];
   load_anchors(T, t0, t1, lane);
-  const float acc = patch_row_score<F32IN>(lv, nl, ld, (size_t)row, t0, t1, normalize, mode, group, out, lane);
+  const float acc = patch_row_score<F32IN, NLMAX>(lv, nl, ld, (size_t)row, t0, t1, normalize, mode, group, out,
+                                                  lane);
   if (mode == 0 && lane == 0) out[row] = acc;
 }
 
@@ -457,12 +461,23 @@ extern "C" int aaclip_patch_scores(int in_dtype, const void* const* levels, int 
     lv.p[i] = levels[i];
   }
   if (rows == 0) return AACLIP_OK;
-  if (in_dtype == AACLIP_F32)
-    patch_scores_kernel<true><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
-        lv, n_levels, ld, T, rows, normalize, mode, mode == 1 ? group : 1, out);
-  else
-    patch_scores_kernel<false><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
-        lv, n_levels, ld, T, rows, normalize, mode, mode == 1 ? group : 1, out);
+  const int grp = mode == 1 ? group : 1;
+  hipStream_t s = (hipStream_t)stream;
+  if (in_dtype == AACLIP_F32) {
+    if (n_levels <= 4)  // C2's 4 levels (and the single-level calls)
+      patch_scores_kernel<true, 4><<<ceil_div(rows, 4), 256, 0, s>>>(lv, n_levels, ld, T, rows, normalize, mode,
+                                                                    grp, out);
+    else
+      patch_scores_kernel<true><<<ceil_div(rows, 4), 256, 0, s>>>(lv, n_levels, ld, T, rows, normalize, mode, grp,
+                                                                 out);
+  } else {
+    if (n_levels <= 4)
+      patch_scores_kernel<false, 4><<<ceil_div(rows, 4), 256, 0, s>>>(lv, n_levels, ld, T, rows, normalize, mode,
+                                                                     grp, out);
+    else
+      patch_scores_kernel<false><<<ceil_div(rows, 4), 256, 0, s>>>(lv, n_levels, ld, T, rows, normalize, mode, grp,
+                                                                  out);
+  }
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
