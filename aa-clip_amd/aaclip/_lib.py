@@ -10,7 +10,7 @@ import ctypes
 import os
 
 LIB_PATH = os.environ.get("AACLIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaaclip_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 F32 = 0
 BF16 = 1
@@ -21,6 +21,7 @@ EPI_GELU = 2
 EPI_LEAKY = 4
 EPI_RESID = 8
 EPI_AUX_BF16 = 16
+EPI_QGELU = 32
 ATTN_CAUSAL = 1
 ATTN_Q_PRESCALED = 2
 

@@ -78,7 +78,8 @@ def _quant_weight_fp8(w: torch.Tensor):
 
 class VisualEngine:
     def __init__(self, vparams: dict, adapter: dict, *, levels=(6, 12, 18, 24), image_adapt_until=6,
-                 image_adapt_weight=0.1, dtype=torch.bfloat16, fold_q_scale=True, fp8_scope="mlp"):
+                 image_adapt_weight=0.1, dtype=torch.bfloat16, fold_q_scale=True, fp8_scope="mlp",
+                 quick_gelu=False):
         """dtype: bfloat16 (perf path), float16 (parity-grade 16-bit path: fp16 MFMA at the
         bf16 rate with 8x finer operand rounding; the weights the OpenAI loader produces
         are fp16-exact, reference model/model.py:366), float32 (fp32-MFMA parity mode) or
@@ -89,7 +90,10 @@ class VisualEngine:
         fp8_scope: "mlp" (default) = c_fc and c_proj in fp8, QKV / attention / out-proj in
         bf16 -- measured at C5: map rel-L2 0.9 % vs the fp32 mode at +24 % images/s over
         bf16; "all" = the four block GEMMs in fp8: +38 % but 8 % map rel-L2 (e4m3 q/k
-        logits amplified by the softmax)."""
+        logits amplified by the softmax).
+        quick_gelu: the MLP activation is QuickGELU (a tower built with quick_gelu=True,
+        reference model/model.py:84) instead of nn.GELU; fused into the c_fc epilogue."""
+        self.act = "quick" if quick_gelu else True
         if dtype not in (torch.bfloat16, torch.float16, torch.float32, FP8):
             raise ValueError("dtype must be bfloat16, float16, float32 or float8_e4m3fn")
         self.fp8 = dtype == FP8
@@ -238,7 +242,7 @@ class VisualEngine:
             ops.tune_gemm(H, blk["w_qkv"], ws["qkv"], bias=blk["b_qkv"])
             ops.tune_gemm(ws["attn"], blk["w_o"], scratch, bias=blk["b_o"], residual=scratch)
         if not self.fp8:
-            ops.tune_gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True)
+            ops.tune_gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=self.act)
             ops.tune_gemm(ws["fc"], blk["w_pr"], scratch, bias=blk["b_pr"], residual=scratch, aux=ws["xb"])
         if self.adapt_until > 0:
             ops.tune_gemm(ws["xb"], self.w_adapt[0], ws["u"], leaky=True)
@@ -279,7 +283,7 @@ class VisualEngine:
 
             def mlp(blk, aux):  # c_fc writes e4m3 + block scales that c_proj consumes directly
                 ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], a8, y_sc=asc)
-                ops.gemm_fp8mx(a8, asc, blk["w_fc"][0], blk["w_fc"][1], f8, out_sc=fsc, bias=blk["b_fc"], gelu=True)
+                ops.gemm_fp8mx(a8, asc, blk["w_fc"][0], blk["w_fc"][1], f8, out_sc=fsc, bias=blk["b_fc"], gelu=self.act)
                 ops.gemm_fp8mx(f8, fsc, blk["w_pr"][0], blk["w_pr"][1], X, bias=blk["b_pr"], residual=X, aux=aux)
         else:
             Hq, Hsc = H, None
@@ -299,12 +303,12 @@ class VisualEngine:
                     a8, asc, f8, fsc = ws["a8"], ws["asc"], ws["f8"], ws["fsc"]
                     ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], a8, y_sc=asc)
                     ops.gemm_fp8mx(a8, asc, blk["w_fc"][0], blk["w_fc"][1], f8, out_sc=fsc, bias=blk["b_fc"],
-                                   gelu=True)
+                                   gelu=self.act)
                     ops.gemm_fp8mx(f8, fsc, blk["w_pr"][0], blk["w_pr"][1], X, bias=blk["b_pr"], residual=X,
                                    aux=aux)
                     return
                 ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], H)
-                ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=True)
+                ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=self.act)
                 ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=aux)
         for i in range(last):
             blk = self.blocks[i]
@@ -522,7 +526,8 @@ class TextEngine:
     """12-block causal text tower; adapted (text_adapter) or plain CLIP projection."""
 
     def __init__(self, params: dict, text_adapter: dict | None, *, text_adapt_until=3, text_adapt_weight=0.1,
-                 dtype=torch.float32):
+                 dtype=torch.float32, quick_gelu=False):
+        self.act = "quick" if quick_gelu else True  # MLP activation (reference model.py:129)
         dev = params["token_embedding.weight"].device
         if dev.type != "cuda":
             raise RuntimeError("TextEngine needs device tensors (no CPU path)")
@@ -584,7 +589,7 @@ class TextEngine:
             ops.attention(qkv, att, n, ctx, self.heads, causal=True)
             ops.gemm(att, blk["w_o"], X, bias=blk["b_o"], residual=X)
             ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], H)
-            ops.gemm(H, blk["w_fc"], fc, bias=blk["b_fc"], gelu=True)
+            ops.gemm(H, blk["w_fc"], fc, bias=blk["b_fc"], gelu=self.act)
             adapt = i < self.adapt_until
             ops.gemm(fc, blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=xb if (adapt and xb is not None) else None)
             nxt = self.blocks[i + 1]["ln1"] if i + 1 < nb else None

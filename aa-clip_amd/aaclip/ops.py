@@ -84,7 +84,9 @@ def _rowmajor(t: torch.Tensor, name: str):
 # ------------------------------------------------------------------------ GEMM
 def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu=False, leaky=False,
          residual=None, aux=None, row_group=0, row_group_out=0, row_offset=0) -> torch.Tensor:
-    """out = epilogue(a @ w.T) — a [M,K], w [N,K] (same dtype), out [M', N]."""
+    """out = epilogue(a @ w.T) — a [M,K], w [N,K] (same dtype), out [M', N].
+    gelu: True = exact erf GELU (nn.GELU), "quick" = QuickGELU x*sigmoid(1.702x)
+    (reference model/transformer.py:46-49)."""
     _dev(a, w, out, bias, residual, aux)
     for t, n in ((a, "a"), (w, "w"), (out, "out")):
         _rowmajor(t, n)
@@ -101,7 +103,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
         raise ValueError("gemm output rows too small for the row remap")
     epi, ldr, ldaux = _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux,
                                       aux_dtype=torch.float16 if a.dtype == torch.float16 else torch.bfloat16)
-    kind = f"gemm N{N} K{K}" + (" leaky" if leaky else "") + (" gelu" if gelu else "") + (" resid" if residual is not None else "")
+    kind = f"gemm N{N} K{K}" + (" leaky" if leaky else "") + (" qgelu" if gelu == "quick" else " gelu" if gelu else "") + (" resid" if residual is not None else "")
     nbytes = (M * K + N * K) * a.element_size() + rows_out * N * out.element_size() * (2 if residual is not None else 1)
     _launch(kind, lambda: gemm_plan(dtag(a), M, N, K) if a.dtype != torch.float32 else "gemm_f32_kernel",
             2.0 * M * N * K, nbytes, "aaclip_gemm", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w),
@@ -279,8 +281,10 @@ def _epilogue_flags(N, rows_out, bias, gelu, leaky, residual, aux, aux_dtype=tor
         if bias.dtype != torch.float32 or bias.numel() != N:
             raise ValueError("bias must be fp32 [N]")
         epi |= _lib.EPI_BIAS
+    if gelu not in (False, True, "quick"):
+        raise ValueError("gelu must be False, True (erf GELU, nn.GELU) or 'quick' (QuickGELU)")
     if gelu:
-        epi |= _lib.EPI_GELU
+        epi |= _lib.EPI_QGELU if gelu == "quick" else _lib.EPI_GELU
     if leaky:
         epi |= _lib.EPI_LEAKY
     ldr = 0

@@ -125,11 +125,27 @@ __device__ __forceinline__ float2_t gelu_fast2(float2_t v) {
   return v * float2_t{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
 }
 
+// QuickGELU (reference transformer.py:46-49: x * sigmoid(1.702 x)). Exact form for the
+// fp32 parity kernel: the same expf/division as torch.sigmoid's fp32 CPU path.
+__device__ __forceinline__ float qgelu_exact(float v) { return v * (1.0f / (1.0f + expf(-1.702f * v))); }
+
+// 16-bit kernels, a column pair in packed f32: v * rcp(1 + 2^(-1.702 log2(e) v)); the
+// argument is clamped to |.| <= 64 (exp2 stays finite, sigmoid is 0/1 to 1e-19 there).
+// |error| vs qgelu_exact <= 2 ulp, far below the 16-bit rounding of the output.
+__device__ __forceinline__ float2_t qgelu_fast2(float2_t v) {
+  constexpr float c = -1.702f * 1.44269504088896340736f;
+  const float2_t w = float2_t{__builtin_amdgcn_fmed3f(v[0] * c, -64.0f, 64.0f),
+                              __builtin_amdgcn_fmed3f(v[1] * c, -64.0f, 64.0f)};
+  const float2_t d = float2_t{__builtin_amdgcn_exp2f(w[0]), __builtin_amdgcn_exp2f(w[1])} + float2_t{1.0f, 1.0f};
+  return v * float2_t{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+}
+
 // Epilogue on one element C[m, n] (m < M checked by the caller).
 __device__ __forceinline__ void epilogue_store1(const GemmArgs& a, int m, int n, float v) {
   const int orow = remap_row(a, m);
   if (a.epi & AACLIP_EPI_BIAS) v += a.bias[n];
   if (a.epi & AACLIP_EPI_GELU) v = gelu_erf(v);
+  if (a.epi & AACLIP_EPI_QGELU) v = qgelu_exact(v);
   if (a.epi & AACLIP_EPI_LEAKY) v = v >= 0.f ? v : 0.01f * v;
   if (a.epi & AACLIP_EPI_RESID) v += a.res[(size_t)orow * a.ldr + n];
   if (a.out_dtype == AACLIP_F32)
@@ -229,6 +245,10 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
         v[j] = acc[i][j] + bias[j];
       if (epi & AACLIP_EPI_GELU) {
         const float2_t lo = gelu_fast2(float2_t{v[j][0], v[j][1]}), hi = gelu_fast2(float2_t{v[j][2], v[j][3]});
+        v[j] = float4_t{lo[0], lo[1], hi[0], hi[1]};
+      }
+      if (epi & AACLIP_EPI_QGELU) {
+        const float2_t lo = qgelu_fast2(float2_t{v[j][0], v[j][1]}), hi = qgelu_fast2(float2_t{v[j][2], v[j][3]});
         v[j] = float4_t{lo[0], lo[1], hi[0], hi[1]};
       }
       if (epi & AACLIP_EPI_LEAKY)
@@ -466,6 +486,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   // the combinations the visual/text engines issue (engine.py)
   EPI_CASE(1, AACLIP_EPI_BIAS)                                        // qkv
   EPI_CASE(1, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)                      // c_fc
+  EPI_CASE(1, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)                     // c_fc, quick_gelu towers
   EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)                     // out-proj, c_proj
   EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)  // c_proj + bf16 copy
   EPI_CASE(0, AACLIP_EPI_LEAKY)                                       // adapters, seg/det proj
@@ -473,6 +494,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   EPI_CASE(0, EPI_REMAP)                                              // patch embedding
   if constexpr (BN / WN == 64) {
     EPI_CASE(2, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)                    // c_fc -> fp8 MX c_proj input
+    EPI_CASE(2, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)
   }
 #undef EPI_CASE
   if (outm == 1)
@@ -740,6 +762,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   } else
       EPI_CASE(true, AACLIP_EPI_BIAS, RM * RN / 2)
       EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU, RM * RN / 2)
+      EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU, RM * RN / 2)
       EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID, RM * RN)
       EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16, RM * RN + RM * RN / 2)
       EPI_CASE(false, AACLIP_EPI_LEAKY, RM * RN)
@@ -923,13 +946,12 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
   EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)                       // out-proj, c_proj
   EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)  // c_proj + bf16 copy
   EPI_CASE(2, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)                        // c_fc -> fp8 MX
+  EPI_CASE(2, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)
 #undef EPI_CASE
   if (outm == 1)
     wave_epilogue<RM, RN, 1, -1, 2>(a, acc, mw, nw, lane);
   else if (outm == 0)
     wave_epilogue<RM, RN, 0, -1, 2>(a, acc, mw, nw, lane);
-  else
-    wave_epilogue<RM, RN, 2, AACLIP_EPI_BIAS | AACLIP_EPI_GELU, 2>(a, acc, mw, nw, lane);
 }
 
 int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
@@ -1171,6 +1193,8 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_BIAS) || ((uintptr_t)bias % 16) == 0);
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_RESID) || (residual && ldr >= N && ldr % 4 == 0));
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_AUX_BF16) || (aux && ldaux >= N && ldaux % 4 == 0));
+  AACLIP_REQUIRE((epilogue & ~63) == 0 && (epilogue & (AACLIP_EPI_GELU | AACLIP_EPI_QGELU)) !=
+                                               (AACLIP_EPI_GELU | AACLIP_EPI_QGELU));
   AACLIP_REQUIRE(row_group >= 0 && (row_group == 0 || row_group_out >= row_group));
   if (M == 0) return AACLIP_OK;
   GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
@@ -1201,6 +1225,8 @@ extern "C" int aaclip_gemm_fp8(int out_dtype, int M, int N, int K, const void* A
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_BIAS) || (bias && ((uintptr_t)bias % 16) == 0));
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_RESID) || (residual && ldr >= N && ldr % 4 == 0));
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_AUX_BF16) || (aux && ldaux >= N && ldaux % 4 == 0));
+  AACLIP_REQUIRE((epilogue & ~63) == 0 && (epilogue & (AACLIP_EPI_GELU | AACLIP_EPI_QGELU)) !=
+                                               (AACLIP_EPI_GELU | AACLIP_EPI_QGELU));
   AACLIP_REQUIRE(row_group >= 0 && (row_group == 0 || row_group_out >= row_group));
   if (M == 0) return AACLIP_OK;
   GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
@@ -1229,7 +1255,10 @@ extern "C" int aaclip_gemm_fp8mx(int out_dtype, int M, int N, int K, const void*
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_BIAS) || (bias && ((uintptr_t)bias % 16) == 0));
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_RESID) || (residual && ldr >= N && ldr % 4 == 0));
   AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_AUX_BF16) || (aux && ldaux >= N && ldaux % 4 == 0));
-  AACLIP_REQUIRE(out_dtype != AACLIP_FP8 || (c_mx && ld_cmx >= M && epilogue == (AACLIP_EPI_BIAS | AACLIP_EPI_GELU)));
+  AACLIP_REQUIRE((epilogue & ~63) == 0 && (epilogue & (AACLIP_EPI_GELU | AACLIP_EPI_QGELU)) !=
+                                               (AACLIP_EPI_GELU | AACLIP_EPI_QGELU));
+  AACLIP_REQUIRE(out_dtype != AACLIP_FP8 || (c_mx && ld_cmx >= M && (epilogue == (AACLIP_EPI_BIAS | AACLIP_EPI_GELU) ||
+                                                         epilogue == (AACLIP_EPI_BIAS | AACLIP_EPI_QGELU))));
   if (M == 0) return AACLIP_OK;
   GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
              out_dtype, 0, 0, 0, 0, 0, g_group_m, g_setprio, g_dbg,

@@ -1,5 +1,5 @@
 // ABI version / target query (include/aaclip.h).
 #include "common.h"
 
-extern "C" int aaclip_abi_version(void) { return 4; }
+extern "C" int aaclip_abi_version(void) { return 5; }
 extern "C" const char* aaclip_arch(void) { return "gfx950"; }

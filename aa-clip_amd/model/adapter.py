@@ -86,7 +86,8 @@ class AdaptedCLIP(nn.Module):
             vp = {"visual." + k: v for k, v in self.image_encoder.state_dict().items()}
             self._vis = VisualEngine(vp, self.image_adapter.state_dict(), levels=self.levels,
                                      image_adapt_until=self.image_adapt_until, image_adapt_weight=self.i_w,
-                                     dtype=self.compute_dtype)
+                                     dtype=self.compute_dtype,
+                                     quick_gelu=self.image_encoder.transformer.quick_gelu)
             self._vis_sig = sig
         return self._vis
 

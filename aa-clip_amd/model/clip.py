@@ -40,25 +40,40 @@ def get_model_config(model_name):
     return None if cfg is None else {k: (dict(v) if isinstance(v, dict) else v) for k, v in cfg.items()}
 
 
+class QuickGELU(nn.Module):
+    """x * sigmoid(1.702 x) (reference model/transformer.py:46-49). Marks a tower built
+    with quick_gelu=True: the engines fuse it into the c_fc epilogue
+    (AACLIP_EPI_QGELU); this eager forward is never on the HIP path."""
+
+    def forward(self, x: torch.Tensor):
+        return x * torch.sigmoid(1.702 * x)
+
+
 class ResidualAttentionBlock(nn.Module):
     """Parameter holder with the names of reference transformer.py:183-219."""
 
-    def __init__(self, d_model: int, n_head: int, mlp_ratio: float = 4.0):
+    def __init__(self, d_model: int, n_head: int, mlp_ratio: float = 4.0, act_layer=nn.GELU):
         super().__init__()
         self.ln_1 = nn.LayerNorm(d_model)
         self.attn = nn.MultiheadAttention(d_model, n_head)
         self.ln_2 = nn.LayerNorm(d_model)
         w = int(d_model * mlp_ratio)
-        self.mlp = nn.Sequential(OrderedDict([("c_fc", nn.Linear(d_model, w)), ("gelu", nn.GELU()),
+        self.mlp = nn.Sequential(OrderedDict([("c_fc", nn.Linear(d_model, w)), ("gelu", act_layer()),
                                               ("c_proj", nn.Linear(w, d_model))]))
 
 
 class Transformer(nn.Module):
-    def __init__(self, width: int, layers: int, heads: int, mlp_ratio: float = 4.0):
+    def __init__(self, width: int, layers: int, heads: int, mlp_ratio: float = 4.0, act_layer=nn.GELU):
         super().__init__()
         self.width, self.layers = width, layers
         self.grad_checkpointing = False
-        self.resblocks = nn.ModuleList([ResidualAttentionBlock(width, heads, mlp_ratio) for _ in range(layers)])
+        self.resblocks = nn.ModuleList([ResidualAttentionBlock(width, heads, mlp_ratio, act_layer)
+                                        for _ in range(layers)])
+
+    @property
+    def quick_gelu(self) -> bool:
+        """The MLP activation the engines fuse: QuickGELU (True) or nn.GELU."""
+        return bool(self.resblocks) and isinstance(self.resblocks[0].mlp.gelu, QuickGELU)
 
     def get_cast_dtype(self) -> torch.dtype:
         return self.resblocks[0].mlp.c_fc.weight.dtype
@@ -68,7 +83,7 @@ class VisionTransformer(nn.Module):
     """Parameter holder with the names of reference transformer.py:320-402."""
 
     def __init__(self, image_size: int, patch_size: int, width: int, layers: int, heads: int,
-                 output_dim: int, mlp_ratio: float = 4.0):
+                 output_dim: int, mlp_ratio: float = 4.0, act_layer=nn.GELU):
         super().__init__()
         self.image_size = (image_size, image_size)
         self.patch_size = (patch_size, patch_size)
@@ -80,7 +95,7 @@ class VisionTransformer(nn.Module):
         self.positional_embedding = nn.Parameter(scale * torch.randn(self.grid_size[0] * self.grid_size[1] + 1, width))
         self.patch_dropout = nn.Identity()  # PatchDropout is the identity in eval (transformer.py:74-75)
         self.ln_pre = nn.LayerNorm(width)
-        self.transformer = Transformer(width, layers, heads, mlp_ratio)
+        self.transformer = Transformer(width, layers, heads, mlp_ratio, act_layer)
         self.embed_dim, self.num_heads = width, heads
         self.ln_post = nn.LayerNorm(width)
         self.proj = nn.Parameter(scale * torch.randn(width, output_dim))
@@ -90,14 +105,16 @@ class CLIP(nn.Module):
     def __init__(self, embed_dim: int, vision_cfg: dict, text_cfg: dict, quick_gelu: bool = False,
                  cast_dtype: Optional[torch.dtype] = None, output_dict: bool = False):
         super().__init__()
-        if quick_gelu:
-            raise NotImplementedError("QuickGELU towers are not on the AA-CLIP path (config uses nn.GELU)")
+        # reference model/model.py:84,129: act_layer = QuickGELU if quick_gelu else nn.GELU
+        act_layer = QuickGELU if quick_gelu else nn.GELU
+        self.quick_gelu = bool(quick_gelu)
         self.output_dict = output_dict
         v = vision_cfg
         self.visual = VisionTransformer(v["image_size"], v["patch_size"], v["width"], v["layers"],
-                                        v["width"] // v.get("head_width", 64), embed_dim, v.get("mlp_ratio", 4.0))
+                                        v["width"] // v.get("head_width", 64), embed_dim, v.get("mlp_ratio", 4.0),
+                                        act_layer)
         t = text_cfg
-        self.transformer = Transformer(t["width"], t["layers"], t["heads"])
+        self.transformer = Transformer(t["width"], t["layers"], t["heads"], act_layer=act_layer)
         self.vocab_size = t["vocab_size"]
         self.token_embedding = nn.Embedding(t["vocab_size"], t["width"])
         self.positional_embedding = nn.Parameter(torch.empty(t["context_length"], t["width"]))
@@ -132,7 +149,8 @@ class CLIP(nn.Module):
                tuple((k, v.data_ptr(), v._version) for k, v in adapter_sd.items()), adapt_until, adapt_weight)
         if self._text_engine is None or self._text_sig != sig:
             self._text_engine = TextEngine(self.text_params(), adapter_sd, text_adapt_until=adapt_until,
-                                           text_adapt_weight=adapt_weight, dtype=torch.float32)
+                                           text_adapt_weight=adapt_weight, dtype=torch.float32,
+                                           quick_gelu=self.transformer.quick_gelu)
             self._text_sig = sig
         return self._text_engine
 
@@ -219,17 +237,24 @@ def create_model(model_name: str, img_size: int, pretrained: Optional[str] = Non
                  force_custom_text: bool = False, force_patch_dropout: Optional[float] = None,
                  force_image_size: Optional[Union[int, Tuple[int, int]]] = None, output_dict: Optional[bool] = None,
                  require_pretrained: bool = False, adapter=False):
-    """Same signature and error behaviour as reference model/clip.py:84-202."""
+    """Same signature and error behaviour as reference model/clip.py:84-202.
+
+    jit=True: the reference scripts the model (torch.jit.script, clip.py:141,199); here
+    the compiled form of the hot path is the engines' hipGraph (predict_cached captures
+    the whole forward + map + score per shape), so the model is returned as built.
+    force_quick_gelu: as in the reference, honoured on the non-OpenAI branch only
+    (clip.py:151-153); the OpenAI branch builds from the config (nn.GELU)."""
     model_name = model_name.replace("/", "-")
     if isinstance(device, str):
         device = torch.device(device)
-    if jit or force_custom_text:
-        raise NotImplementedError("jit / custom-text CLIP variants are not on the AA-CLIP path")
+    if force_custom_text:
+        raise NotImplementedError("custom-text CLIP variants are not on the AA-CLIP path")
+    if jit:
+        logging.info("jit=True: the HIP engines capture the forward in a hipGraph (predict_cached); "
+                     "no TorchScript pass")
     model_cfg = get_model_config(model_name)
     if model_cfg is None:
         raise RuntimeError(f"Model config for {model_name} not found.")
-    if force_quick_gelu:
-        model_cfg["quick_gelu"] = True
     if pretrained and pretrained.lower() == "openai":
         logging.info(f"Loading pretrained {model_name} from OpenAI.")
         model_cfg["vision_cfg"]["image_size"] = img_size
@@ -238,6 +263,8 @@ def create_model(model_name: str, img_size: int, pretrained: Optional[str] = Non
         resize_pos_embed(sd, model)
         model.load_state_dict(sd, strict=True)
     else:
+        if force_quick_gelu:
+            model_cfg["quick_gelu"] = True
         if force_image_size is not None:
             model_cfg["vision_cfg"]["image_size"] = force_image_size
         model = CLIP(**model_cfg)

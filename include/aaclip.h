@@ -44,6 +44,10 @@ extern "C" {
 #define AACLIP_EPI_RESID 8     /* + residual[row, n] (fp32; may alias C)    */
 #define AACLIP_EPI_AUX_BF16 16 /* also store a 16-bit copy of the result: fp16 when
                                   in_dtype is AACLIP_F16, bf16 otherwise      */
+#define AACLIP_EPI_QGELU 32    /* QuickGELU v * sigmoid(1.702 v), applied where GELU
+                                  is (reference model/transformer.py:46-49; the
+                                  towers built with quick_gelu=True, model.py:84,129);
+                                  exclusive with AACLIP_EPI_GELU               */
 
 /* ABI version (bumped on any signature change; 2 = MX fp8 LayerNorm outputs, 3 = fp16 dtype,
  * aaclip_patch_logits, any-size blur_upsample) and the target. */

@@ -46,6 +46,13 @@ def gelu_erf(x: np.ndarray) -> np.ndarray:
     return (F32(0.5) * x * (F32(1.0) + _erf(x * F32(1.0 / np.sqrt(2.0))).astype(F32))).astype(F32)
 
 
+def quick_gelu(x: np.ndarray) -> np.ndarray:
+    """QuickGELU x * sigmoid(1.702 x) (transformer.py:46-49; towers built with quick_gelu=True,
+    model.py:84,129)."""
+    x = x.astype(F32, copy=False)
+    return (x * (F32(1.0) / (F32(1.0) + np.exp(F32(-1.702) * x)))).astype(F32)
+
+
 def leaky_relu(x: np.ndarray, slope: float = 0.01) -> np.ndarray:
     """nn.LeakyReLU() default slope 0.01 (adapter_modules.py:9,20)."""
     return np.where(x >= 0, x, x * F32(slope)).astype(F32)
@@ -91,12 +98,13 @@ def attention(h: np.ndarray, p: dict, prefix: str, heads: int, causal: bool) -> 
     return linear(o, p[prefix + ".out_proj.weight"], p[prefix + ".out_proj.bias"])
 
 
-def resblock(x: np.ndarray, p: dict, prefix: str, heads: int, causal: bool = False) -> np.ndarray:
-    """ResidualAttentionBlock.forward (transformer.py:239-258)."""
+def resblock(x: np.ndarray, p: dict, prefix: str, heads: int, causal: bool = False,
+             quick: bool = False) -> np.ndarray:
+    """ResidualAttentionBlock.forward (transformer.py:239-258); quick: QuickGELU MLP."""
     h = layer_norm(x, p[prefix + ".ln_1.weight"], p[prefix + ".ln_1.bias"])
     x = x + attention(h, p, prefix + ".attn", heads, causal)
     h = layer_norm(x, p[prefix + ".ln_2.weight"], p[prefix + ".ln_2.bias"])
-    h = gelu_erf(linear(h, p[prefix + ".mlp.c_fc.weight"], p[prefix + ".mlp.c_fc.bias"]))
+    h = (quick_gelu if quick else gelu_erf)(linear(h, p[prefix + ".mlp.c_fc.weight"], p[prefix + ".mlp.c_fc.bias"]))
     x = x + linear(h, p[prefix + ".mlp.c_proj.weight"], p[prefix + ".mlp.c_proj.bias"])
     return x.astype(F32)
 
@@ -129,7 +137,7 @@ def patch_embed(sd: dict, x: np.ndarray) -> np.ndarray:
 
 def visual_forward(sd: dict, img_ad: dict, x: np.ndarray, levels=(6, 12, 18, 24),
                    image_adapt_until: int = 6, image_adapt_weight: float = 0.1,
-                   return_trace: bool = False):
+                   return_trace: bool = False, quick: bool = False):
     """AdaptedCLIP.forward (adapter.py:67-112) -> (seg_tokens list [B,P,768] unit rows, det [B,768])."""
     x = patch_embed(sd, x.astype(F32))
     B = x.shape[0]
@@ -139,7 +147,7 @@ def visual_forward(sd: dict, img_ad: dict, x: np.ndarray, levels=(6, 12, 18, 24)
     tokens = []
     trace = []
     for i in range(24):
-        x = resblock(x, sd, f"visual.transformer.resblocks.{i}", 16)
+        x = resblock(x, sd, f"visual.transformer.resblocks.{i}", 16, quick=quick)
         if i < image_adapt_until:
             x = adapter_blend(x, img_ad[f"layer_adapters.{i}.fc.0.weight"], image_adapt_weight)
         if return_trace:
@@ -161,13 +169,13 @@ def visual_forward(sd: dict, img_ad: dict, x: np.ndarray, levels=(6, 12, 18, 24)
 
 
 def encode_text(sd: dict, txt_ad: dict | None, tokens: np.ndarray, text_adapt_until: int = 3,
-                text_adapt_weight: float = 0.1) -> np.ndarray:
+                text_adapt_weight: float = 0.1, quick: bool = False) -> np.ndarray:
     """AdaptedCLIP.encode_text (adapter.py:114-145) when txt_ad is given,
     else CLIP.encode_text (model.py:190-201)."""
     tokens = np.asarray(tokens).astype(np.int64)
     x = sd["token_embedding.weight"][tokens] + sd["positional_embedding"]
     for i in range(12):
-        x = resblock(x, sd, f"transformer.resblocks.{i}", 12, causal=True)
+        x = resblock(x, sd, f"transformer.resblocks.{i}", 12, causal=True, quick=quick)
         if txt_ad is not None and i < text_adapt_until:
             x = adapter_blend(x, txt_ad[f"{i}.fc.0.weight"], text_adapt_weight)
     x = layer_norm(x, sd["ln_final.weight"], sd["ln_final.bias"])

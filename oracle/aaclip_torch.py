@@ -33,14 +33,16 @@ import torch.nn.functional as F
 WIDTH, HEADS, LAYERS, PATCH = 1024, 16, 24, 14
 
 
-def prepare(sd: dict, img_ad: dict, levels=(6, 12, 18, 24), image_adapt_until: int = 6) -> dict:
-    """State dicts (numpy or torch, reference key names) -> fp32 CPU tensors."""
+def prepare(sd: dict, img_ad: dict, levels=(6, 12, 18, 24), image_adapt_until: int = 6,
+            quick_gelu: bool = False) -> dict:
+    """State dicts (numpy or torch, reference key names) -> fp32 CPU tensors.
+    quick_gelu: the tower's MLP activation is QuickGELU (model.py:84, transformer.py:46-49)."""
     t = lambda a: torch.as_tensor(np.asarray(a) if not isinstance(a, torch.Tensor) else a).float().contiguous()  # noqa: E731
     w = {"conv": t(sd["visual.conv1.weight"]).reshape(WIDTH, -1), "cls": t(sd["visual.class_embedding"]),
          "pos": t(sd["visual.positional_embedding"]),
          "ln_pre": (t(sd["visual.ln_pre.weight"]), t(sd["visual.ln_pre.bias"])),
          "ln_post": (t(sd["visual.ln_post.weight"]), t(sd["visual.ln_post.bias"])),
-         "levels": tuple(levels), "blocks": []}
+         "levels": tuple(levels), "blocks": [], "quick": bool(quick_gelu)}
     for i in range(LAYERS):
         p = f"visual.transformer.resblocks.{i}."
         w["blocks"].append({k: t(sd[p + n]) for k, n in (
@@ -59,7 +61,11 @@ def prepare(sd: dict, img_ad: dict, levels=(6, 12, 18, 24), image_adapt_until: i
     return w
 
 
-def _block(x: torch.Tensor, b: dict) -> torch.Tensor:
+def _act(h: torch.Tensor, quick: bool) -> torch.Tensor:
+    return h * torch.sigmoid(1.702 * h) if quick else F.gelu(h)
+
+
+def _block(x: torch.Tensor, b: dict, quick: bool = False) -> torch.Tensor:
     """ResidualAttentionBlock (transformer.py:239-258) on token-major [B, N, D]."""
     B, N, D = x.shape
     h = F.layer_norm(x, (D,), b["ln1w"], b["ln1b"], 1e-5)
@@ -70,7 +76,7 @@ def _block(x: torch.Tensor, b: dict) -> torch.Tensor:
     o = (a @ v).transpose(1, 2).reshape(B, N, D)
     x = x + F.linear(o, b["wo"], b["bo"])
     h = F.layer_norm(x, (D,), b["ln2w"], b["ln2b"], 1e-5)
-    return x + F.linear(F.gelu(F.linear(h, b["wfc"], b["bfc"])), b["wpr"], b["bpr"])
+    return x + F.linear(_act(F.linear(h, b["wfc"], b["bfc"]), quick), b["wpr"], b["bpr"])
 
 
 def visual_forward(w: dict, x: torch.Tensor, image_adapt_weight: float = 0.1):
@@ -84,7 +90,7 @@ def visual_forward(w: dict, x: torch.Tensor, image_adapt_weight: float = 0.1):
     x = F.layer_norm(x, (WIDTH,), *w["ln_pre"], 1e-5)
     taps = []
     for i, b in enumerate(w["blocks"][:max(w["levels"])]):
-        x = _block(x, b)
+        x = _block(x, b, w["quick"])
         if i < len(w["adapt"]):  # adapter.py:92-99
             u = F.leaky_relu(x @ w["adapt"][i].T, 0.01)
             u = u * x.norm(dim=-1, keepdim=True) / u.norm(dim=-1, keepdim=True)

@@ -18,6 +18,9 @@ every fixture here is "reference code on synthetic weights". Outputs:
                     adapter blend, similarity map incl. train branch, metrics_eval)
   golden_c5.npz     config-C5 shapes: 448 px (1025 tokens), 6 levels [4..24],
                     relu=True projections, Medical-domain map, B=1
+  golden_quick.npz  towers built with force_quick_gelu=True (clip.py:151-153 -> QuickGELU,
+                    transformer.py:46-49): visual/text block KATs, text encoding, B=1
+                    336 px grid/det/score/map (`python tests/golden/make_golden.py quick`)
   golden_518.npz    the reference's default test size (test.py:111, results/test.log:1-3):
                     518 px (37x37 grid, 1370 tokens), 4 levels, B=1, both domains
                     (`python tests/golden/make_golden.py 518` regenerates only this file)
@@ -56,7 +59,7 @@ def t(a):
     return torch.from_numpy(np.ascontiguousarray(a))
 
 
-def build_reference(relu=False, levels=(6, 12, 18, 24), img_size=336):
+def build_reference(relu=False, levels=(6, 12, 18, 24), img_size=336, quick_gelu=False):
     prev = os.getcwd()
     os.chdir(REF)  # the reference resolves ./dataset/metadata relative to cwd
     try:
@@ -66,7 +69,7 @@ def build_reference(relu=False, levels=(6, 12, 18, 24), img_size=336):
         os.chdir(prev)
     # the random-init branch ignores img_size; force_image_size sets the grid (clip.py:159-161)
     clip = create_model("ViT-L-14-336", img_size, pretrained=None, device="cpu",
-                        force_image_size=img_size if img_size != 336 else None)
+                        force_image_size=img_size if img_size != 336 else None, force_quick_gelu=quick_gelu)
     sd = synth.clip_state_dict(SEED, img_size=img_size)
     clip.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
     clip.eval()
@@ -282,9 +285,41 @@ def main_518():
     print("golden_518.npz", os.path.getsize(os.path.join(HERE, "golden_518.npz")))
 
 
+@torch.no_grad()
+def main_quick():
+    """force_quick_gelu=True (the reference honours it on the non-OpenAI branch,
+    model/clip.py:151-153): every MLP runs QuickGELU (transformer.py:46-49)."""
+    clip, model, sd, img_ad, txt_ad = build_reference(quick_gelu=True)
+    assert type(clip.transformer.resblocks[0].mlp.gelu).__name__ == "QuickGELU"
+    import forward_utils as fu
+    text = np.load(os.path.join(HERE, "golden_text.npz"))
+    g = np.random.Generator(np.random.Philox(key=SEED + 7))
+    xv = g.standard_normal((17, 2, 1024), dtype=np.float32)
+    xt = (g.standard_normal((77, 1, 768), dtype=np.float32) * 0.5).astype(np.float32)
+    # inputs are regenerated by the test from the same Philox key; outputs thinned to keep the file small
+    out = dict(clip_sha=np.array(synth.state_checksum(sd)),
+               vblock_y=model.image_encoder.transformer.resblocks[3](t(xv), attn_mask=None)[0].numpy()[::2],
+               tblock_y=clip.transformer.resblocks[1](t(xt), attn_mask=clip.attn_mask)[0].numpy()[::4],
+               tok_abnormal=text["bottle_tok_abnormal"],
+               enc_abnormal_adapted=model.encode_text(t(text["bottle_tok_abnormal"])).numpy(),
+               enc_abnormal_clip=clip.encode_text(t(text["bottle_tok_abnormal"])).numpy())
+    T = t(text["bottle_T_adapted"])
+    x = synth.images(SEED, 1, 336)
+    seg, det = model(t(x))
+    m = torch.cat([fu.calculate_similarity_map(f, T, 336, test=True, domain="Industrial") for f in seg], 1).sum(1)
+    out.update(image_sha=np.array(synth.state_checksum({"x": x})), T=text["bottle_T_adapted"],
+               grid_A=np.stack([(100.0 * (f @ T)).numpy() for f in seg], axis=1).astype(np.float32),
+               det=det.numpy(), score=((det @ T)[:, 1].numpy() + 1) / 2, map_ind_sub=m.numpy()[:, ::7, ::7])
+    np.savez_compressed(os.path.join(HERE, "golden_quick.npz"), **out)
+    print("golden_quick.npz", os.path.getsize(os.path.join(HERE, "golden_quick.npz")))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["518"]:
         main_518()
+    elif sys.argv[1:] == ["quick"]:
+        main_quick()
     else:
         main()
         main_518()
+        main_quick()

@@ -280,3 +280,39 @@ def test_predict_cached_replays_graph_bit_identical(dev, weights):
             m0, s0 = eng.predict(x, T, "Industrial", streams=streams)
             assert torch.equal(m1, m0) and torch.equal(s1, s0), (rep, B)
     assert len(eng._graph_cache) == 2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+def test_quick_gelu_towers_parity(dev, weights, dtype):
+    """Towers built with force_quick_gelu=True (reference clip.py:151-153): QuickGELU
+    fused into every c_fc epilogue, visual and text, vs the reference's golden_quick.npz.
+    fp32 / fp16 hold the map contract (1e-3 + 1e-2 |ref|) with 0 sure-margin label
+    flips; bf16 as test_visual_bf16_parity (flips bounded)."""
+    import os
+    q = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_quick.npz"))
+    eng = _visual(weights, dtype, quick_gelu=True)
+    x = torch.from_numpy(synth.images(111, 1, 336)).to(dev)
+    T = torch.from_numpy(q["T"]).to(dev)
+    seg, det = eng.forward(x)
+    grid = np.stack([(100.0 * (f @ T)).cpu().numpy() for f in seg], axis=1)
+    sure = np.abs(q["grid_A"][..., 1] - q["grid_A"][..., 0]) > 1e-3
+    flips = int((grid.argmax(-1) != q["grid_A"].argmax(-1))[sure].sum())
+    maps, score = eng.predict(x, T, "Industrial")
+    got = maps.cpu().numpy()[:, ::7, ::7]
+    err = np.abs(got - q["map_ind_sub"])
+    print(dtype, "quick_gelu map max abs", err.max(), "flips", flips, "of", int(sure.sum()))
+    assert (err <= 1e-3 + 1e-2 * np.abs(q["map_ind_sub"])).all()
+    np.testing.assert_allclose(score.cpu().numpy(), q["score"], atol=1e-3)
+    assert flips <= (0 if dtype != torch.bfloat16 else 0.01 * sure.sum())
+    # the erf-GELU engine on the same weights is visibly off this golden
+    plain = _visual(weights, dtype).predict(x, T, "Industrial")[0].cpu().numpy()[:, ::7, ::7]
+    assert np.abs(plain - q["map_ind_sub"]).max() > 10 * max(err.max(), 1e-4)
+    if dtype == torch.float16:
+        return
+    sd, _, ta, _ = weights
+    tp = {k: v for k, v in sd.items() if not k.startswith("visual.")}
+    tol = 1e-5 if dtype == torch.float32 else 5e-2
+    for ad, key in ((ta, "adapted"), (None, "clip")):
+        enc = TextEngine(tp, ad, dtype=dtype, quick_gelu=True).encode(torch.from_numpy(q["tok_abnormal"]).to(dev))
+        ref = q[f"enc_abnormal_{key}"]
+        np.testing.assert_allclose(enc.cpu().numpy(), ref, atol=tol * max(1.0, np.abs(ref).max()), rtol=tol * 10)

@@ -213,7 +213,8 @@ def test_gemm_fp8mx_odd_rows_last_row(dev, mx_variant, M):
             ops.gemm_fp8mx(a8, odd, w8, sw, out)
 
 
-def test_gemm_fp8mx_gelu_fp8_output_chain(dev, mx_variant):
+@pytest.mark.parametrize("act", [True, "quick"])
+def test_gemm_fp8mx_gelu_fp8_output_chain(dev, mx_variant, act):
     """c_fc -> c_proj hand-off in fp8: the GELU epilogue writes e4m3 + its own e8m0 block
     scales, which feed the next MX GEMM directly (no quantisation pass)."""
     torch.manual_seed(11)
@@ -228,9 +229,10 @@ def test_gemm_fp8mx_gelu_fp8_output_chain(dev, mx_variant):
     wpr8, spr = _wq(wpr)
     f8 = torch.empty(M, F, device=dev, dtype=FP8)
     fsc = ops.mx_scales(M, F, dev)
-    ops.gemm_fp8mx(h8, hsc, wfc8, sfc, f8, out_sc=fsc, bias=bfc, gelu=True)
+    ops.gemm_fp8mx(h8, hsc, wfc8, sfc, f8, out_sc=fsc, bias=bfc, gelu=act)
     # the fp8 GELU output vs GELU of the exact product of the quantised operands
-    g_ref = torch.nn.functional.gelu(_mx_dequant(h8, hsc) @ (wfc8.double() * sfc.double()[:, None]).T + bfc.double())
+    pre = _mx_dequant(h8, hsc) @ (wfc8.double() * sfc.double()[:, None]).T + bfc.double()
+    g_ref = pre * torch.sigmoid(1.702 * pre) if act == "quick" else torch.nn.functional.gelu(pre)
     g = _mx_dequant(f8, fsc)
     blk = g_ref.abs().view(M, F // 64, 64).amax(-1).repeat_interleave(64, dim=1)
     assert ((g - g_ref).abs() <= 2.0 ** -4 * g_ref.abs() + blk * 2.0 ** -8 + 1e-4).all()

@@ -37,6 +37,29 @@ def test_create_model_error_conventions():
     assert m.visual.positional_embedding.shape == (1025, 1024)
 
 
+def test_create_model_quick_gelu_and_jit(monkeypatch):
+    """force_quick_gelu builds QuickGELU towers on the non-OpenAI branch only (reference
+    clip.py:151-153; the OpenAI branch builds from the config, clip.py:107-142); the
+    engines read the activation off the modules. jit=True is accepted (the hipGraph of
+    predict_cached is the compiled path) and returns the model."""
+    import model.clip as clip
+    from model.adapter import AdaptedCLIP
+    m = clip.create_model("ViT-L-14-336", 336, pretrained=None, force_quick_gelu=True, jit=True)
+    assert isinstance(m, clip.CLIP) and m.quick_gelu
+    assert m.visual.transformer.quick_gelu and m.transformer.quick_gelu
+    assert isinstance(m.visual.transformer.resblocks[5].mlp.gelu, clip.QuickGELU)
+    x = torch.linspace(-6, 6, 101)
+    torch.testing.assert_close(m.transformer.resblocks[0].mlp.gelu(x), x * torch.sigmoid(1.702 * x))
+    sd = synth.clip_state_dict(111)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)  # same parameter names
+    assert AdaptedCLIP(m, relu=False).image_encoder.transformer.quick_gelu
+    plain = clip.create_model("ViT-L-14-336", 336, pretrained=None)
+    assert not plain.quick_gelu and not plain.visual.transformer.quick_gelu
+    monkeypatch.setattr(clip, "load_openai_state_dict", lambda path: {k: torch.from_numpy(v) for k, v in sd.items()})
+    o = clip.create_model("ViT-L-14-336", 336, pretrained="openai", force_quick_gelu=True)
+    assert not o.visual.transformer.quick_gelu and not o.transformer.quick_gelu
+
+
 def test_adapted_clip_modality_error():
     from model.adapter import AdaptedCLIP
     from model.clip import create_model

@@ -75,6 +75,53 @@ def test_gemm_bf16_out_epilogue(dev, gelu, M, N):
     assert (err <= 8e-3 * ref.abs() + 2e-3).all(), err.max().item()
 
 
+def _qgelu(x):
+    return x * torch.sigmoid(1.702 * x)  # reference model/transformer.py:46-49
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8, 9])
+def test_gemm_quick_gelu_epilogue(dev, dtype, variant):
+    """AACLIP_EPI_QGELU (towers built with quick_gelu=True) on every tile family, 16-bit
+    and fp32 outputs, a ragged last M-tile; float64 reference. The fp32 kernel keeps
+    the exact expf form: 1e-5 relative."""
+    if dtype == torch.float32 and variant:
+        pytest.skip("the fp32 kernel has one tile family")
+    M, N, K = 3 * 577, 4096, 1024
+    torch.manual_seed(variant)
+    a = torch.randn(M, K, device=dev).to(dtype)
+    w = (torch.randn(N, K, device=dev) * K ** -0.5).to(dtype)
+    bias = torch.randn(N, device=dev) * 0.5
+    ref = _qgelu(a.double() @ w.double().T + bias.double())
+    _lib.call("aaclip_set_gemm_variant", variant)
+    try:
+        for odt in ((torch.float32,) if dtype == torch.float32 else (dtype, torch.float32)):
+            out = torch.full((M, N), float("nan"), device=dev, dtype=odt)
+            ops.gemm(a, w, out, bias=bias, gelu="quick")
+            err = (out.double() - ref).abs()
+            tol = 1e-5 * ref.abs() + 1e-5 if odt == torch.float32 and dtype == torch.float32 else \
+                (8e-3 * ref.abs() + 2e-3 if odt != torch.float32 else 1e-3 * ref.abs() + 1e-3)
+            assert not torch.isnan(out).any()
+            assert (err <= tol).all(), (odt, err.max().item())
+    finally:
+        _lib.call("aaclip_set_gemm_variant", 0)
+    with pytest.raises(ValueError):
+        ops.gemm(a, w, out, bias=bias, gelu="tanh")
+
+
+def test_gemm_gelu_flags_exclusive(dev):
+    """GELU and QuickGELU together, or an unknown epilogue bit, are rejected by the C ABI."""
+    a = torch.randn(64, 64, device=dev).bfloat16()
+    w = torch.randn(256, 64, device=dev).bfloat16()
+    out = torch.empty(64, 256, device=dev)
+    bias = torch.zeros(256, device=dev)
+    for epi in (_lib.EPI_BIAS | _lib.EPI_GELU | _lib.EPI_QGELU, 128):
+        with pytest.raises(RuntimeError):
+            _lib.call("aaclip_gemm", _lib.BF16, _lib.F32, 64, 256, 64, a.data_ptr(), 64, w.data_ptr(), 64,
+                      out.data_ptr(), 256, epi, bias.data_ptr(), None, 0, None, 0, 0, 0, 0,
+                      torch.cuda.current_stream().cuda_stream)
+
+
 @pytest.mark.parametrize("variant", [3, 5])
 @pytest.mark.parametrize("M,N,K", [(18464, 4096, 1024), (4100, 3072, 4096), (513, 256, 192), (9232, 1024, 4096)])
 def test_gemm_8phase_race_screen(dev, variant, M, N, K):
