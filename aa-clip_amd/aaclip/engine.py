@@ -161,6 +161,7 @@ class VisualEngine:
         self.relu = r_det
         self.w_seg = [cdt(t) for t in self.w_seg[:-1]] + [cdt(torch.cat([self.w_seg[-1], w_det], 0))]
         self._ws = {}
+        self.map_fused = os.environ.get("AACLIP_MAP_FUSED", "1") != "0"
         self.poison = False  # tests: fill new workspaces with NaN (read-before-write screen)
 
     # ------------------------------------------------------------------ workspace
@@ -226,6 +227,7 @@ class VisualEngine:
                         t.fill_(float("nan"))
                     else:
                         t.view(torch.uint8).fill_(0xFF)
+        ws["bandcnt"] = ops.map_band_counters(B, S, dev)  # zero; every fused map launch leaves it zero
         if TUNE and cdt != torch.float32:
             self._tune(ws)
         return ws
@@ -365,14 +367,18 @@ class VisualEngine:
         P = out[0].shape[0] // B
         return [y.view(B, P, EMBED) for y in out], det
 
-    @staticmethod
-    def _tail(seg_raw, det_raw, ws, T, out_map, out_score, k, s):
+    def _tail(self, seg_raw, det_raw, ws, T, out_map, out_score, k, s):
         """Anomaly map + image score of one chunk from its projections. Two passes over
         segbuf (the level features, then the det rows): measured 4 % faster than the one
         pass of aaclip_anomaly_map_score (62.7 vs 65.1 us at B = 32, tools/map_ab.py), whose
         16-row workgroups stream at 4.6 TB/s where the one-row-per-wave map pass reaches
-        6.4; the one-pass entry stays in the ABI, bit-identical (tests)."""
-        ops.anomaly_map(seg_raw, T, out_map, ws["grid"], g=ws["g"], ksize=k, sigma=s)
+        6.4; the one-pass entry stays in the ABI, bit-identical (tests). The map itself is
+        one launch (aaclip_anomaly_map_fused: blur + upsample in the stream's tail) unless
+        AACLIP_MAP_FUSED=0 (the two-launch form, same bits)."""
+        if self.map_fused:
+            ops.anomaly_map_fused(seg_raw, T, out_map, ws["grid"], ws["bandcnt"], g=ws["g"], ksize=k, sigma=s)
+        else:
+            ops.anomaly_map(seg_raw, T, out_map, ws["grid"], g=ws["g"], ksize=k, sigma=s)
         ops.image_score(det_raw, out_map.shape[0], ws["P"], ws["partial"], det=ws["det"], T=T, score=out_score)
 
     def _chunk_streams(self, n: int):

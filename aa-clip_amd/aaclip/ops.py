@@ -513,6 +513,33 @@ def anomaly_map(levels, T, out, grid_ws, *, g, ksize, sigma, normalize=True):
     return out
 
 
+def map_band_counters(B: int, S: int, device) -> torch.Tensor:
+    """Zeroed band counters for anomaly_map_fused (B * ceil(S / 8) int32); every fused call
+    leaves them zero again. One set per concurrently running call (per chunk workspace)."""
+    return torch.zeros(B * ((S + 7) // 8), device=device, dtype=torch.int32)
+
+
+def anomaly_map_fused(levels, T, out, grid_ws, counters, *, g, ksize, sigma):
+    """anomaly_map in one launch (aaclip_anomaly_map_fused): same bits; counters from
+    map_band_counters(B, S)."""
+    _dev(*levels, T, out, grid_ws, counters)
+    B, S, S2 = out.shape
+    rows, C = levels[0].shape
+    if rows != B * g * g or S != S2 or grid_ws.numel() < rows or grid_ws.dtype != torch.float32:
+        raise ValueError("anomaly_map_fused shape mismatch (grid_ws: fp32 >= [B*g*g])")
+    if counters.dtype != torch.int32 or counters.numel() < B * ((S + 7) // 8) or not out.is_contiguous():
+        raise ValueError("anomaly_map_fused: counters int32 >= B*ceil(S/8), contiguous output")
+    for t in levels:
+        if t.shape != (rows, C) or t.stride(0) != levels[0].stride(0) or t.dtype != levels[0].dtype:
+            raise ValueError("levels must share shape, dtype and stride")
+    arr = _level_array(levels)
+    nb = len(levels) * rows * C * levels[0].element_size() + C * 2 * 4 + B * S * S * 4 + 2 * rows * 4
+    _launch("anomaly_map", "anomaly_map (map_fused_kernel)", 0.0, nb, "aaclip_anomaly_map_fused",
+            dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(T), B, g, C, S, ksize, float(sigma),
+            _ptr(grid_ws), _ptr(counters), _ptr(out), _stream())
+    return out
+
+
 def image_score(det_raw, batch, n_patch, partial, det=None, T=None, score=None, normalize=True):
     _dev(det_raw, partial, det, T, score)
     _rowmajor(det_raw, "det_raw")

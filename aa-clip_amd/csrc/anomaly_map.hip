@@ -173,16 +173,15 @@ constexpr int kMaxC = 8;  // channels of the train branch (anchors), softmax ove
 // lambdas: no FMA contraction). K = ksize at compile time for the domains' 7 and 9
 // (tap loads issued together), -1 = any ksize at run time, 0 = no blur.
 // LDS: C * (2 * xrows + brows) * g floats, sized by the host for the band.
+// The band body is a device function: blur_upsample_kernel runs it for one (image, band)
+// per workgroup, map_fused_kernel for the bands its workgroup completes (same bits).
 template <int C, int K>
-__global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, float* out, int g, int S,
-                                                           int ksize_rt, Gauss gw, int softmax, float scale,
-                                                           int xrows, int brows) {
+__device__ __forceinline__ void blur_band(const float* grid, float* out, int b, int band, int g, int S,
+                                          int ksize_rt, const Gauss& gw, int softmax, float scale, int xrows,
+                                          int brows, float* smem, int lane) {
 #pragma clang fp contract(off)
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int ksize = K >= 0 ? K : ksize_rt;
-  const int lane = threadIdx.x;
-  const int b = blockIdx.y;
-  const int y0 = blockIdx.x * kBand;
+  const int y0 = band * kBand;
   const int y1 = min(y0 + kBand, S);
   const int r_lo = (int)(scale * (float)y0);
   const int r_hi = min((int)(scale * (float)(y1 - 1)) + 1, g - 1);
@@ -327,6 +326,96 @@ __global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, fl
         }
       }
     }
+  }
+}
+
+template <int C, int K>
+__global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, float* out, int g, int S,
+                                                           int ksize_rt, Gauss gw, int softmax, float scale,
+                                                           int xrows, int brows) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  blur_band<C, K>(grid, out, blockIdx.y, blockIdx.x, g, S, ksize_rt, gw, softmax, scale, xrows, brows, smem,
+                  threadIdx.x);
+}
+
+// Source grid rows [x_lo, x_hi] one output band reads (blur_band: the bilinear taps'
+// rows r_lo..r_hi and their blur neighbourhood, clamped; reflected indices stay inside).
+__device__ __forceinline__ void band_rows(int band, int g, int S, int ksize, float scale, int& x_lo, int& x_hi) {
+  const int y0 = band * kBand;
+  const int y1 = min(y0 + kBand, S);
+  const int r_lo = (int)(scale * (float)y0);
+  const int r_hi = min((int)(scale * (float)(y1 - 1)) + 1, g - 1);
+  const int r = ksize / 2;
+  x_lo = ksize > 0 ? max(0, r_lo - r) : r_lo;
+  x_hi = ksize > 0 ? min(g - 1, r_hi + r) : r_hi;
+}
+
+// The whole test-branch map in ONE launch: workgroup (r, b) streams the g patch rows of
+// grid row r of image b through every level (patch_row_score, the bits of
+// patch_scores_kernel; 8 waves, each wave one patch position at a time), writes the
+// level-summed scores to grid, and then counts itself into every output band whose
+// source rows [x_lo, x_hi] hold row r (one device-scope atomic per band). The workgroup
+// whose count completes a band computes that band (blur_band, the bits of
+// blur_upsample_kernel) and zeroes its counter for the next launch: no workgroup ever
+// waits for another, and the blur + upsample runs in the tail of the stream instead of
+// a second launch. Ordering: each wave's grid stores complete (vmcnt) before the
+// barrier, wave 0 releases at agent scope before its atomics, a band's computing wave
+// acquires at agent scope before it reads the grid (the grid rows come from other
+// workgroups, other XCDs' L2s). cnt: batch * nbands int32, zero before the first launch.
+constexpr int kFusedWaves = 8;
+constexpr int kMaxBands = 128;  // out_size <= 1024
+
+template <bool F32IN, int NLMAX, int K>
+__global__ __launch_bounds__(64 * kFusedWaves, NLMAX <= 4 ? 4 : 2) void map_fused_kernel(LevelPtrs lv, int nl, int64_t ld,
+                                                                    const float* T, int g, int S, int ksize_rt,
+                                                                    Gauss gw, float scale, int xrows, int brows,
+                                                                    int nbands, float* grid, int* cnt, float* out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // kFusedWaves band-staging slices
+  __shared__ int ready[kMaxBands];
+  __shared__ int nready;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = blockIdx.x, b = blockIdx.y;
+  const int ksize = K >= 0 ? K : ksize_rt;
+  {
+    float4_t t0[3], t1[3];
+    load_anchors(T, t0, t1, lane);
+    for (int j = wid; j < g; j += kFusedWaves) {
+      const size_t row = ((size_t)b * g + r) * g + j;
+      const float acc = patch_row_score<F32IN, NLMAX>(lv, nl, ld, row, t0, t1, 1, 0, 1, nullptr, lane);
+      if (lane == 0) grid[row] = acc;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's grid stores are in L2
+  __syncthreads();
+  if (wid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    int n = 0;
+    for (int k0 = 0; k0 < nbands; k0 += 64) {
+      const int k = k0 + lane;
+      bool done = false;
+      if (k < nbands) {
+        int x_lo, x_hi;
+        band_rows(k, g, S, ksize, scale, x_lo, x_hi);
+        if (x_lo <= r && r <= x_hi) {
+          int* c = cnt + (size_t)b * nbands + k;
+          const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          done = old + 1 == x_hi - x_lo + 1;
+          if (done) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      const uint64_t m = __builtin_amdgcn_ballot_w64(done);
+      if (done) ready[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = k;
+      n += __builtin_popcountll(m);
+    }
+    if (lane == 0) nready = n;
+  }
+  __syncthreads();
+  const int n = nready;
+  if (wid < n) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    float* slice = smem + (size_t)wid * (2 * xrows + brows) * g;
+    for (int i = wid; i < n; i += kFusedWaves)
+      blur_band<1, K>(grid, out, b, ready[i], g, S, ksize_rt, gw, 0, scale, xrows, brows, slice, lane);
   }
 }
 
@@ -548,6 +637,52 @@ extern "C" int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n
                                normalize, 0, 0, grid_ws, stream);
   if (rc) return rc;
   return aaclip_blur_upsample(grid_ws, out, batch, 1, g, out_size, ksize, sigma, 0, stream);
+}
+
+extern "C" int aaclip_anomaly_map_fused(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
+                                        const float* T, int batch, int g, int channels, int out_size, int ksize,
+                                        float sigma, float* grid_ws, int* band_counters, float* out,
+                                        void* stream) {
+  AACLIP_REQUIRE(in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16);
+  AACLIP_REQUIRE(levels && T && grid_ws && band_counters && out && batch > 0);
+  AACLIP_REQUIRE(channels == 768 && ld >= channels && ld % 4 == 0);
+  AACLIP_REQUIRE(n_levels >= 1 && n_levels <= kMaxLevels);
+  AACLIP_REQUIRE(g >= 2 && g <= 64 && out_size >= 2 && ceil_div(out_size, kBand) <= kMaxBands);
+  AACLIP_REQUIRE(ksize >= 0 && ksize <= 15 && (ksize == 0 || (ksize % 2 == 1 && ksize / 2 < g)));
+  LevelPtrs lv{};
+  for (int i = 0; i < n_levels; ++i) {
+    AACLIP_REQUIRE(levels[i] != nullptr);
+    lv.p[i] = levels[i];
+  }
+  const Gauss gw = ksize > 0 ? gaussian_weights(ksize, sigma) : Gauss{};
+  const float scale = (float)(g - 1) / (float)(out_size - 1);
+  const int span = (int)(scale * (float)(kBand - 1)) + 4;  // as launch_blur_upsample
+  const int brows = min(g, span);
+  const int xrows = min(g, brows + 2 * (ksize / 2));
+  const size_t lds = (size_t)kFusedWaves * (2 * xrows + brows) * g * sizeof(float);
+  AACLIP_REQUIRE(lds <= 64 * 1024);
+  const int nbands = ceil_div(out_size, kBand);
+  const dim3 grd(g, batch);
+  hipStream_t s = (hipStream_t)stream;
+  const bool f32 = in_dtype == AACLIP_F32, nl4 = n_levels <= 4;
+#define MF_LAUNCH(F, NLM, K)                                                                                     \
+  map_fused_kernel<F, NLM, K><<<grd, 64 * kFusedWaves, lds, s>>>(lv, n_levels, ld, T, g, out_size, ksize, gw,    \
+                                                                 scale, xrows, brows, nbands, grid_ws,           \
+                                                                 band_counters, out)
+#define MF_K(F, NLM)                \
+  if (ksize == 7) MF_LAUNCH(F, NLM, 7);      \
+  else if (ksize == 9) MF_LAUNCH(F, NLM, 9); \
+  else if (ksize == 0) MF_LAUNCH(F, NLM, 0); \
+  else MF_LAUNCH(F, NLM, -1);
+  if (f32) {
+    if (nl4) { MF_K(true, 4) } else { MF_K(true, kMaxLevels) }
+  } else {
+    if (nl4) { MF_K(false, 4) } else { MF_K(false, kMaxLevels) }
+  }
+#undef MF_K
+#undef MF_LAUNCH
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
 }
 
 extern "C" int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld, const float* T,

@@ -357,7 +357,8 @@ def map_from_profile(p1, p2):
     m = p1["by_op"]["anomaly_map"]
     gbs = m["bytes"] / (m["ms"] * 1e-3) / 1e9
     traffic, src = pmc_traffic("map")
-    out = {"kernel": "aaclip_anomaly_map (patch_scores_kernel + blur_upsample_kernel)", "bound": "hbm",
+    kern = next((k for k in p1["by_kernel"] if k.startswith("anomaly_map")), "anomaly_map")
+    out = {"kernel": "aaclip_" + kern, "bound": "hbm",
            "unit": "GB/s", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
            "traffic": traffic, "traffic_source": src, "avg_launch_us": m["avg_launch_us"],
            "bytes_per_launch": m["bytes"] / m["launches"],
@@ -425,6 +426,8 @@ def roofline_map_isolated(eng, ws, T, reps=50):
     S = ws["map"].shape[-1]
     g = ws["g"]
     t_all = time_launches(lambda: ops.anomaly_map(seg, T, ws["map"], ws["grid"], g=g, ksize=7, sigma=1.0), reps, s)
+    t_fused = time_launches(lambda: ops.anomaly_map_fused(seg, T, ws["map"], ws["grid"], ws["bandcnt"], g=g, ksize=7,
+                                                          sigma=1.0), reps, s)
     t_ps = time_launches(lambda: ops.patch_scores(seg, T, ws["grid"][:rows]), reps, s)
     t_bu = time_launches(lambda: ops.blur_upsample(ws["grid"][:rows].view(B, 1, g, g), ws["map"].view(B, 1, S, S),
                                                    ksize=7, sigma=1.0), reps, s)
@@ -437,6 +440,8 @@ def roofline_map_isolated(eng, ws, T, reps=50):
             "unit": "GB/s", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic, "traffic_source": src, "avg_launch_us": round(t_all * 1e3, 2),
             "bytes_per_launch": nbytes,
+            "fused_one_launch": {"kernel": "map_fused_kernel", "us": round(t_fused * 1e3, 2),
+                                 "GBs": round(nbytes / (t_fused * 1e-3) / 1e9, 1)},
             "stage1_patch_scores": {"us": round(t_ps * 1e3, 2), "bytes": read1 + rows * 4,
                                     "GBs": round((read1 + rows * 4) / (t_ps * 1e-3) / 1e9, 1)},
             "stage2_blur_upsample": {"us": round(t_bu * 1e3, 2), "bytes": write2 + rows * 4,

@@ -313,6 +313,20 @@ int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n_levels, in
                        void* stream);
 
 /*
+ * aaclip_anomaly_map (normalised features) in ONE launch: one workgroup per (image,
+ * grid row) streams that row's patch positions through every level into grid_ws
+ * (>= batch*g*g fp32), then counts itself into the output bands (kBand = 8 output
+ * rows) whose blur + bilinear source rows include its row; the workgroup that
+ * completes a band computes it. Same bits as aaclip_anomaly_map. band_counters:
+ * batch * ceil(out_size / 8) int32, ZERO before the first call; every call leaves them
+ * zero (one counter set per concurrently running call). out_size <= 1024, g <= 64.
+ * Replaces: test.py:86-93 + forward_utils.py:196-213.
+ */
+int aaclip_anomaly_map_fused(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
+                             const float* T, int batch, int g, int channels, int out_size, int ksize,
+                             float sigma, float* grid_ws, int* band_counters, float* out, void* stream);
+
+/*
  * Image-level score: det[b] = mean_p normalize(det_raw[b*n_patch+p]) and
  * score[b] = (det[b] . T[:,1] + 1) / 2. partial: workspace
  * [batch, ceil(n_patch/16), channels] fp32 (fixed-order reduction, deterministic).

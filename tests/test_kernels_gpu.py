@@ -522,6 +522,32 @@ def test_anomaly_map_equals_stages(dev, dt, B, g, S, L, dom):
         assert torch.equal(out, ref[:, 0])
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,g,S,L,k", [(32, 24, 336, 4, 7), (3, 24, 336, 4, 9), (2, 37, 518, 4, 7),
+                                       (2, 37, 518, 4, 9), (2, 32, 448, 6, 9), (5, 8, 41, 1, 7),
+                                       (1, 24, 336, 8, 7), (4, 12, 1000, 2, 0), (3, 20, 200, 3, 13)])
+def test_anomaly_map_fused_equals_two_pass(dev, dt, B, g, S, L, k):
+    """aaclip_anomaly_map_fused (one launch: per-(image, grid row) workgroups, the band
+    that a workgroup completes computed by it) is bit-identical to the two-launch
+    aaclip_anomaly_map at the C2 (B = 32), 518, C5 and ragged shapes, every ksize path
+    (7, 9, none, run-time 13) -- and leaves its band counters zero, so repeated launches
+    (graph replays) stay identical."""
+    torch.manual_seed(B * g + S + L)
+    lv = [torch.randn(B * g * g, 768, device=dev).to(dt) for _ in range(L)]
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev), dim=0).contiguous()
+    sg = 1.0 + 0.1 * k
+    ref = torch.empty(B, S, S, device=dev)
+    ops.anomaly_map(lv, T, ref, torch.empty(B * g * g, device=dev), g=g, ksize=k, sigma=sg)
+    cnt = ops.map_band_counters(B, S, dev)
+    grid = torch.full((B * g * g,), float("nan"), device=dev)
+    for _ in range(3):
+        out = torch.full((B, S, S), float("nan"), device=dev)
+        ops.anomaly_map_fused(lv, T, out, grid, cnt, g=g, ksize=k, sigma=sg)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        assert int(cnt.abs().sum()) == 0
+
+
 # ----------------------------------------------------------------------------- NaN propagation
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("where", ["q", "k", "v"])
