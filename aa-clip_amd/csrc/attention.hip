@@ -278,6 +278,100 @@ __device__ __forceinline__ void attn_tile_split(const char* kt_lds, const h16x8_
   for (int ks = 0; ks < 2; ++ks) l_acc[1] = mfma16(ones, p1[ks], l_acc[1]);
 }
 
+// Full 64-key tile for two 16-query blocks, speculative exponentials (tiles after the
+// first): both blocks' Kᵀ·Q first, then block 0's p = exp2(S' - m) formed against the
+// CURRENT running max before the deferred-max check -- the exponentials depend only on
+// the scores, so they issue beside block 1's Kᵀ·Q MFMAs instead of waiting for a max
+// tree, a ballot and a branch. Both blocks' lane maxima feed ONE ballot; on its rare
+// taken path each block rescales exactly as attn_tile_split does (a block that does not
+// move gets d = 0: alpha = 1, st - 0, the same bits) and block 0's p is formed again
+// from the shifted scores. On the common path the executed arithmetic is the split
+// tile's, so the results are bit-identical to it. A p formed against a stale max may be
+// +inf (S' - m > 128); it is discarded on that path.
+template <bool H16>
+__device__ __forceinline__ void attn_tile_spec(const char* kt_lds, const h16x8_t<H16> (&qf)[2][2],
+                                               float4_t (&ot)[2][4], float (&m_run)[2], float4_t (&l_acc)[2],
+                                               int g, int c) {
+  using V8 = h16x8_t<H16>;
+  using E = h16_t<H16>;
+  const char* vt_lds = kt_lds + KT * 128;
+  V8 kf[4][2];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) kf[kb][ks] = *(const V8*)(kt_lds + swz(kb * 16 + c, ks * 4 + g));
+  auto qk = [&](int qb, float4_t (&st)[4]) {
+    const float nm = -m_run[qb];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) st[kb] = float4_t{nm, nm, nm, nm};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) st[kb] = mfma16(kf[kb][ks], qf[qb][ks], st[kb]);
+  };
+  auto expo = [&](const float4_t (&st)[4], V8 (&pf)[2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      V8 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = (E)__builtin_amdgcn_exp2f(st[2 * ks][i]);
+        v[4 + i] = (E)__builtin_amdgcn_exp2f(st[2 * ks + 1][i]);
+      }
+      pf[ks] = v;
+    }
+  };
+  auto rescale = [&](int qb, float4_t (&st)[4], float mx) {
+    mx = max_over_groups(mx);
+    const float d = mx > kRescaleLog2 ? mx : 0.f;
+    m_run[qb] += d;
+    const float alpha = __builtin_amdgcn_exp2f(-d);
+    l_acc[qb][0] *= alpha;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ot[qb][db][e] *= alpha;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st[kb][i] -= d;
+  };
+  float4_t s0[4], s1[4];
+  V8 p0[2], p1[2];
+  qk(0, s0);
+  qk(1, s1);
+  expo(s0, p0);
+  // pin the speculative exponentials ahead of the branch (hipcc would otherwise sink
+  // them into the not-taken path, behind the ballot)
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(p0[ks]));
+  const float mx0 = tile_lane_max<4>(s0), mx1 = tile_lane_max<4>(s1);
+  if (__builtin_amdgcn_ballot_w64(mx0 > kRescaleLog2 || mx1 > kRescaleLog2) != 0) {
+    rescale(0, s0, mx0);
+    rescale(1, s1, mx1);
+    expo(s0, p0);
+  }
+  expo(s1, p1);
+  const V8 ones = {(E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) l_acc[0] = mfma16(ones, p0[ks], l_acc[0]);
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int qq = c >> 2, pp = c & 3;
+      const int chunk = db * 2 + (pp >> 1);
+      const int r0 = ks * 32 + 4 * g + qq;
+      const short4_t lo = tr_read(vt_lds + swz(r0, chunk) + (pp & 1) * 8);
+      const short4_t hi = tr_read(vt_lds + swz(r0 + 16, chunk) + (pp & 1) * 8);
+      const V8 vf = __builtin_bit_cast(V8, short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      ot[0][db] = mfma16(vf, p0[ks], ot[0][db]);
+      ot[1][db] = mfma16(vf, p1[ks], ot[1][db]);
+    }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) l_acc[1] = mfma16(ones, p1[ks], l_acc[1]);
+}
+
 #ifndef ATTN_STAGES
 #define ATTN_STAGES 3  // K/V ring depth (LDS: ATTN_STAGES x 16 KiB per workgroup)
 #endif
@@ -303,7 +397,7 @@ __device__ __forceinline__ void wait_barrier(bool deep) {
 // QB 16-query blocks per wave, NW waves per workgroup (QT = 16 * QB * NW queries),
 // NS-stage K/V ring. Every wave reads the whole K and V tile from LDS, so queries
 // per wave set the LDS bytes per FLOP: QB = 4 halves them against QB = 2.
-template <bool H16, int QB, int NW, int NS, bool SPLIT>
+template <bool H16, int QB, int NW, int NS, int SPLIT>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_kernel(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int batch, int N, int H, int flags,
     uint8_t* __restrict__ out_mx, int64_t ld_mx) {
@@ -434,7 +528,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
   for (; t < nfull; ++t) {
     const bool deep = advance();
     if (active) {
-      if constexpr (SPLIT && QB == 2)
+      if constexpr (SPLIT == 2 && QB == 2) {
+        if (t == 0)
+          attn_tile_split<H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, g, c, true);
+        else
+          attn_tile_spec<H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, g, c);
+      } else if constexpr (SPLIT == 1 && QB == 2)
         attn_tile_split<H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, g, c, t == 0);
       else
         attn_tile<4, QB, false, H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g,
@@ -724,11 +823,12 @@ __global__ __launch_bounds__(256, 2) void attn_f32_kernel(const float* __restric
 
 // 1 = 4 waves x 32 queries (3-stage ring, 3 workgroups per CU), 2 = 2 waves x 64
 // queries (2-stage ring, 4 workgroups per CU: half the LDS bytes per FLOP), 3 = 1
-// with the phase-split full tile (attn_tile_split: 3-6 % faster, the default)
+// with the phase-split full tile (attn_tile_split: 3-6 % faster, the default), 4 = 3
+// with speculative exponentials after tile 0 (attn_tile_spec, same bits)
 constexpr int kAttnDefault = 3;
 int g_attn_variant = 0;
 
-template <bool H16, int QB, int NW, int NS, bool SPLIT = false>
+template <bool H16, int QB, int NW, int NS, int SPLIT = 0>
 void launch_attn(const uint16_t* q, uint16_t* o, int batch, int seq, int heads, int flags, uint8_t* mx, int64_t ld_mx,
                  hipStream_t s) {
   const long nwg = (long)ceil_div(seq, 16 * QB * NW) * batch * heads;
@@ -738,7 +838,7 @@ void launch_attn(const uint16_t* q, uint16_t* o, int batch, int seq, int heads, 
 }  // namespace
 
 extern "C" int aaclip_set_attn_variant(int variant) {
-  AACLIP_REQUIRE(variant >= 0 && variant <= 3);
+  AACLIP_REQUIRE(variant >= 0 && variant <= 4);
   g_attn_variant = variant;
   return AACLIP_OK;
 }
@@ -762,11 +862,13 @@ extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch
     uint8_t* mx = dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr;
     if (dtype == AACLIP_F16) {
       if (v == 2) launch_attn<true, 4, 2, 2>(q, o, batch, seq, heads, flags, nullptr, 0, s);
-      else if (v == 3) launch_attn<true, 2, 4, ATTN_STAGES, true>(q, o, batch, seq, heads, flags, nullptr, 0, s);
+      else if (v == 3) launch_attn<true, 2, 4, ATTN_STAGES, 1>(q, o, batch, seq, heads, flags, nullptr, 0, s);
+      else if (v == 4) launch_attn<true, 2, 4, ATTN_STAGES, 2>(q, o, batch, seq, heads, flags, nullptr, 0, s);
       else launch_attn<true, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, nullptr, 0, s);
     } else {
       if (v == 2) launch_attn<false, 4, 2, 2>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
-      else if (v == 3) launch_attn<false, 2, 4, ATTN_STAGES, true>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
+      else if (v == 3) launch_attn<false, 2, 4, ATTN_STAGES, 1>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
+      else if (v == 4) launch_attn<false, 2, 4, ATTN_STAGES, 2>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
       else launch_attn<false, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
     }
   } else {

@@ -275,7 +275,7 @@ def test_attention_bf16(dev, B, N, H, causal):
     assert err < 3e-2, err
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 4])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (2, 73, 4, False),
                                           (1, 200, 2, False)])
@@ -317,6 +317,38 @@ def test_attention_spiky_rows(dev):
         ops.attention(x, out, B, N, H)
         ref = _attn_ref(x, B, N, H, False)
         assert (out.double() - ref).abs().max().item() < (2e-2 if dt == torch.bfloat16 else 1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,N,H,spikes", [(2, 577, 16, 0), (1, 1025, 16, 0), (2, 577, 4, 6), (1, 1370, 2, 9)])
+def test_attention_spec_equals_split(dev, dt, B, N, H, spikes):
+    """Variant 4 (speculative exponentials, attn_tile_spec) runs the split tile's arithmetic on
+    its common path and the same per-block rescale on the rare one, so its output is
+    bit-identical to variant 3's; `spikes` keys get a huge logit for every query of head 0
+    (spread over the tiles, so the deferred max moves at several tiles, some where only one
+    of a wave's two query blocks moves), forcing the re-formed exponentials."""
+    g = torch.Generator(device=dev).manual_seed(N + spikes)
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev, generator=g) * 1.5
+    if spikes:
+        qkv[:, :64] = 1.0
+        for i in range(spikes):
+            row = (N // spikes) * i + 70 + 13 * i
+            qkv[min(row, B * N - 1), H * 64:H * 64 + 64] = 2.0 + i
+        qkv[: N // 3, :64] = 0.5  # queries of one block shift less than the others'
+    x = qkv.to(dt)
+    outs = []
+    for v in (3, 4):
+        out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
+        _lib.call("aaclip_set_attn_variant", v)
+        try:
+            ops.attention(x, out, B, N, H)
+        finally:
+            _lib.call("aaclip_set_attn_variant", 0)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    err = (outs[1].double() - _attn_ref(x, B, N, H, False)).abs().max().item()
+    assert err < (3e-2 if dt == torch.bfloat16 else 4e-3), err
 
 
 SL2 = 0.125 * 1.4426950408889634  # log2(e)/sqrt(64), what the engine folds into the Q projection

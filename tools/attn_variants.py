@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--seqs", default="577,1025,1370")
     ap.add_argument("--eager", type=int, default=0, help="launch each variant this many times, no timing")
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved timing rounds (all variants per round)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     dt = {"bf16": torch.bfloat16, "fp16": torch.float16}[a.dtype]
@@ -48,13 +49,20 @@ def main():
         for v in [int(x) for x in a.variants.split(",")]:  # warm-up: the first timed launches read high
             _lib.call("aaclip_set_attn_variant", v)
             graph_time(lambda: ops.attention(qkv, out, a.batch, N, H), reps=5)
-        for v in [int(x) for x in a.variants.split(",")]:
-            _lib.call("aaclip_set_attn_variant", v)
-            t = graph_time(lambda: ops.attention(qkv, out, a.batch, N, H), reps=20)
-            ops.attention(small, osmall, 2, N, H)
-            err = (osmall.double() - ref).abs().max().item()
-            tf = 4.0 * a.batch * N * N * H * 64 / (t * 1e-6) / 1e12
-            print(f"N={N} variant={v} {t:8.2f} us {tf:7.1f} TFLOP/s  max err {err:.2e}", flush=True)
+        first = None
+        for r in range(a.rounds):
+            for v in [int(x) for x in a.variants.split(",")]:
+                _lib.call("aaclip_set_attn_variant", v)
+                t = graph_time(lambda: ops.attention(qkv, out, a.batch, N, H), reps=20)
+                ops.attention(small, osmall, 2, N, H)
+                err = (osmall.double() - ref).abs().max().item()
+                ops.attention(qkv, out, a.batch, N, H)
+                if first is None:
+                    first = out.clone()
+                same = torch.equal(first.view(torch.int16), out.view(torch.int16))
+                tf = 4.0 * a.batch * N * N * H * 64 / (t * 1e-6) / 1e12
+                print(f"N={N} round={r} variant={v} {t:8.2f} us {tf:7.1f} TFLOP/s  max err {err:.2e}"
+                      f"  bits={'same' if same else 'DIFF'}", flush=True)
     _lib.call("aaclip_set_attn_variant", 0)
 
 
