@@ -202,7 +202,7 @@ __device__ __forceinline__ uint4 pair_h16(const float4_t& lo, const float4_t& hi
 // SCALED: 0 = none, 1 = a_scale[row] * w_scale[col] (fp8 per-row), 2 = w_scale[col]
 // only (fp8 MX: the activation block scales were applied by the MFMA).
 // H16: the 16-bit storage of OUTM 1 and of the aux copy is fp16 (else bf16).
-template <int RM, int RN, int OUTM, int EPI, int SCALED, bool H16 = false>
+template <int RM, int RN, int OUTM, int EPI, int SCALED, bool H16 = false, int PD = 2>
 __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
                                               int lane) {
   static_assert(RN % 2 == 0, "column tiles are paired");
@@ -222,16 +222,24 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
 #pragma unroll
     for (int j = 0; j < RN; ++j) wsc[j] = *(const float4_t*)(a.w_scale + ncol + 16 * j);
   }
-  float4_t res[2][RN];
+  // residual rows in a PD-deep register ring: tile-row i + PD - 1 is requested before
+  // tile-row i is used. PD = 4 on the 8-phase kernel (244 VGPRs, no spill) measured
+  // 0.4 % SLOWER in the two-stream step than PD = 2 (224 VGPRs): above 224 the 8-wave
+  // workgroup leaves no room on a SIMD for a 64-VGPR row-kernel wave of the other chunk.
+  static_assert(PD >= 2 && PD <= RM, "residual ring depth");
+  float4_t res[PD][RN];
   auto load_res = [&](int i, float4_t (&dst)[RN]) {
     const float* src = a.res + (size_t)out_row(min(mw + 16 * i + fr, a.M - 1)) * a.ldr + ncol;
 #pragma unroll
     for (int j = 0; j < RN; ++j) dst[j] = *(const float4_t*)(src + 16 * j);
   };
-  if (epi & AACLIP_EPI_RESID) load_res(0, res[0]);
+  if (epi & AACLIP_EPI_RESID) {
+#pragma unroll
+    for (int i = 0; i < PD - 1 && i < RM; ++i) load_res(i, res[i]);
+  }
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
-    if ((epi & AACLIP_EPI_RESID) && i + 1 < RM) load_res(i + 1, res[(i + 1) & 1]);
+    if ((epi & AACLIP_EPI_RESID) && i + PD - 1 < RM) load_res(i + PD - 1, res[(i + PD - 1) % PD]);
     float4_t v[RN];
     float asc = 1.f;
     if constexpr (SCALED == 1) asc = a.a_scale[min(mw + 16 * i + fr, a.M - 1)];
@@ -254,7 +262,7 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
       if (epi & AACLIP_EPI_LEAKY)
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[j][t] = v[j][t] >= 0.f ? v[j][t] : 0.01f * v[j][t];
-      if (epi & AACLIP_EPI_RESID) v[j] += res[i & 1][j];
+      if (epi & AACLIP_EPI_RESID) v[j] += res[i % PD][j];
     }
     if (a.dbg & 2) {  // diagnostic: everything but the global stores
 #pragma unroll
@@ -954,6 +962,131 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
     wave_epilogue<RM, RN, 0, -1, 2>(a, acc, mw, nw, lane);
 }
 
+// ======================= two-workgroups-per-CU bf16 kernel (256x128 tile, K-step 32)
+// The 8-phase kernel fills a CU with ONE workgroup (8 waves x 224+ VGPRs, 128 KiB LDS):
+// while its waves run the epilogue (bias / GELU / residual, then the stores) the CU's
+// matrix cores idle -- measured 2.3 ms of the 13.9 ms two-stream C2 step
+// (tools/epi_bound.py). This kernel keeps the same 128x64 wave tile (so the same
+// wave_epilogue) in 4-wave workgroups of 72 KiB LDS and <= 256 VGPRs: two workgroups
+// share each CU, one wave of each per SIMD, and one's epilogue runs beside the other's
+// main loop. K-step 32 (64-B LDS rows) so a 3-stage ring fits the 80 KiB share; the
+// ring's end-of-step wait is COUNTED (the next stage's 6 DMA pieces per wave stay in
+// flight across the barrier). LDS image: lane (fr, fq) reads 16-B chunk fq of row r,
+// stored at physical chunk fq ^ ((r >> 2) & 2) -- conflict-free for ds_read_b128's
+// lane groups (searched exhaustively); the swizzle is applied on the DMA source side.
+// Same K order as every other 16-bit family (K ascending, one fp32 accumulator per
+// output), so the results are bit-identical to them.
+template <bool H16>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_pp2_kernel(GemmArgs a) {
+  using V8 = h16x8_t<H16>;
+  constexpr int BM = 256, BN = 128, TM = 128, TN = 64, RM = 8, RN = 4;
+  constexpr int A_BYTES = BM * 64, STAGE = (BM + BN) * 64;  // 16 KiB + 8 KiB
+  constexpr int NS = 3;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  int tm, tn;
+  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const auto ars = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)((uint32_t)a.M * (uint32_t)a.lda * 2u),
+                                                     0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, (int)((uint32_t)a.N * (uint32_t)a.ldw * 2u),
+                                                     0x00020000);
+  // DMA piece = 16 rows x 64 B; lane -> row lane/4 of the piece, physical chunk lane%4,
+  // logical (source) chunk (lane%4) ^ ((row >> 2) & 2). Wave w fills A pieces w, w+4, w+8,
+  // w+12 and B pieces w, w+4. Rows past M / N read as zeros (buffer range check).
+  const int prow = lane >> 2;
+  const int lchunk = ((lane & 3) ^ ((prow >> 2) & 2)) * 8;  // elements
+  int a_vo[4], b_vo[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a_vo[i] = ((m0 + (i * 4 + wid) * 16 + prow) * (int)a.lda + lchunk) * 2;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) b_vo[i] = ((n0 + (i * 4 + wid) * 16 + prow) * (int)a.ldw + lchunk) * 2;
+  auto stage = [&](int kt, int buf) {
+    char* dst = smem + buf * STAGE;
+    const int ko = kt * 64;  // bytes
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, LDS_PTR(dst + (i * 4 + wid) * 1024), 16, a_vo[i], ko, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + A_BYTES + (i * 4 + wid) * 1024), 16, b_vo[i], ko,
+                                               0, 0);
+  };
+  const int sw = (fq ^ ((fr >> 2) & 2)) << 4;
+  const int a_rd = (wr * TM + fr) * 64 + sw, b_rd = A_BYTES + (wc * TN + fr) * 64 + sw;
+  float4_t acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+  const int nk = a.K / 32;
+  stage(0, 0);
+  if (nk > 1) stage(1, 1);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // stage kt landed; kt+1 may fly
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of stage kt landed, stage kt-1 read
+    if (kt + 2 < nk) stage(kt + 2, cur == 0 ? 2 : cur - 1);
+    const char* st = smem + cur * STAGE;
+    V8 bf[RN];
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bf[j] = *(const V8*)(st + b_rd + j * 1024);
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const V8 af = *(const V8*)(st + a_rd + i * 1024);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = mfma16(bf[j], af, acc[i][j]);
+    }
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  const int mw = m0 + wr * TM, nw = n0 + wc * TN;
+  if (a.dbg & 1) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  const bool bf16_out = a.out_dtype != AACLIP_F32;
+  const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
+#define EPI_CASE(BF, E)                                                   \
+  if (bf16_out == (BF) && key == (E)) {                                   \
+    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane);   \
+    return;                                                               \
+  }
+  EPI_CASE(true, AACLIP_EPI_BIAS)
+  EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)
+  EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)
+  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)
+  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)
+  EPI_CASE(false, AACLIP_EPI_LEAKY)
+#undef EPI_CASE
+  if (bf16_out)
+    wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane);
+  else
+    wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane);
+}
+
+template <bool H16>
+int launch_bf16_pp2(GemmArgs a, hipStream_t s) {
+  if (a.N % 128 || a.K % 32) return AACLIP_ERR_ARG;
+  a.tiles_m = ceil_div(a.M, 256);
+  a.tiles_n = a.N / 128;
+  const size_t lds = 3 * (256 + 128) * 64;
+  static unsigned attr_dev = 0;
+  if (!lds_attr_once((const void*)gemm_bf16_pp2_kernel<H16>, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
+  gemm_bf16_pp2_kernel<H16><<<a.tiles_m * a.tiles_n, 256, lds, s>>>(a);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
 int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
@@ -1062,7 +1195,7 @@ int pinned_family(int dtype, int M, int N, int K) {
 thread_local int t_concurrent = 0;
 
 enum Kern { KERN_256x256 = 1, KERN_256x128 = 2, KERN_8PH = 3, KERN_8PH_PERSIST = 5, KERN_320x256 = 8,
-            KERN_128x128 = 9 };
+            KERN_128x128 = 9, KERN_PP2 = 10 };
 
 // The kernel a 16-bit GEMM of this shape launches: the A/B variant hook, else a pin,
 // else the concurrent-chunk rule, else the per-shape heuristic (fewer tile rounds
@@ -1086,6 +1219,9 @@ int choose16(int dtype, int M, int N, int K, bool fits) {
       if (N % 256 == 0 && fits) return KERN_8PH_PERSIST;
       break;
     case 9: return KERN_128x128;  // 128x128 everywhere (A/B)
+    case 10:  // two workgroups per CU, 256x128 tile, K-step 32
+      if (fits && K % 32 == 0) return KERN_PP2;
+      break;
     case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
       if (N % 256 == 0) return KERN_320x256;
       break;
@@ -1111,6 +1247,7 @@ int dispatch16(GemmArgs a, hipStream_t s) {
     case KERN_8PH_PERSIST: return launch_bf16_8ph<H16, true>(a, s);
     case KERN_320x256: return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
     case KERN_128x128: return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);
+    case KERN_PP2: return launch_bf16_pp2<H16>(a, s);
     default: return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
   }
 }
@@ -1129,14 +1266,16 @@ extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
     case KERN_8PH_PERSIST: return "gemm_bf16_8ph_kernel<256,256,persistent>";
     case KERN_320x256: return "gemm_bf16_kernel<320,256,2,4>";
     case KERN_128x128: return "gemm_bf16_kernel<128,128,2,2>";
+    case KERN_PP2: return "gemm_bf16_pp2_kernel<256,128>";
     default: return "gemm_bf16_kernel<256,128,4,2>";
   }
 }
 
 extern "C" int aaclip_gemm_pin(int in_dtype, int M, int N, int K, int family) {
   AACLIP_REQUIRE((in_dtype == AACLIP_BF16 || in_dtype == AACLIP_F16) && M > 0 && N > 0 && K > 0);
-  AACLIP_REQUIRE(family == 0 || family == 1 || family == 2 || family == 3 || family == 8 || family == 9);
-  AACLIP_REQUIRE(family == 0 || family == 2 || N % 256 == 0);
+  AACLIP_REQUIRE(family == 0 || family == 1 || family == 2 || family == 3 || family == 8 || family == 9 ||
+                 family == 10);
+  AACLIP_REQUIRE(family == 0 || family == 2 || family == 10 || N % 256 == 0);
   std::lock_guard<std::mutex> lk(g_pin_mu);
   const int n = g_npins.load(std::memory_order_relaxed);
   for (int i = 0; i < n; ++i)
@@ -1167,10 +1306,10 @@ extern "C" int aaclip_set_gemm_variant(int variant) {
   // bits 0-3: tile family (0 default = per-shape choice, 1 = 256x256, 2 = 256x128, 3/4 = 256x256
   // 8-phase ping-pong everywhere / for N >= 2048, 5 = persistent 8-phase, 6 = MX fp8 on the
   // 256x256 LDS-DMA kernel instead
-  // of its 8-phase default, 8 = 320x256 everywhere); bits 4-7: tile-order
+  // of its 8-phase default, 8 = 320x256 everywhere, 9 = 128x128, 10 = two-workgroup 256x128); bits 4-7: tile-order
   // group height (0 = 8); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 2048 || fam > 9 || fam == 7) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 2048 || fam > 10 || fam == 7) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 8;
   g_setprio = (variant >> 8) & 1;

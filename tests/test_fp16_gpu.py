@@ -22,7 +22,7 @@ H16 = torch.float16
 
 
 # ----------------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 8, 9, 10])
 @pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (18464, 4096, 1024)])
 def test_gemm_f16_variants(dev, variant, M, N, K):
     """Every 16-bit tile family (default per-shape choice, 256x256, 256x128, 8-phase,
@@ -43,7 +43,7 @@ def test_gemm_f16_variants(dev, variant, M, N, K):
     assert (out.double() - ref).abs().max().item() < 1e-4 * ref.abs().max().item() + 1e-5
 
 
-@pytest.mark.parametrize("variant", [0, 3, 5, 8, 9])
+@pytest.mark.parametrize("variant", [0, 3, 5, 8, 9, 10])
 def test_gemm_f16_epilogues(dev, variant):
     """fp16 output (bias, bias + GELU), fp32 residual in place + fp16 aux copy, LeakyReLU."""
     torch.manual_seed(11)

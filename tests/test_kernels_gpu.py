@@ -31,11 +31,12 @@ def test_gemm_bf16_plain(dev, M, N, K):
     assert err < 1e-3 * ref.abs().max().item() + 1e-4, err
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 5, 8, 9])
+@pytest.mark.parametrize("variant", [1, 2, 3, 5, 8, 9, 10])
 @pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (2000, 256, 64),
                                    (18464, 3072, 1024), (577 * 40, 1024, 512), (300, 512, 128)])
 def test_gemm_bf16_variants(dev, variant, M, N, K):
-    """Forced bf16 tile families (256x256, 256x128, 256x256 8-phase ping-pong, 320x256);
+    """Forced bf16 tile families (256x256, 256x128, 256x256 8-phase ping-pong, 320x256,
+    128x128, the two-workgroup 256x128 K-step-32 kernel);
     the default picks between the last two per shape and is covered by every other GEMM test."""
     from aaclip import _lib
     if variant in (1, 3, 5, 8) and N % 256:
@@ -80,7 +81,7 @@ def _qgelu(x):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8, 9, 10])
 def test_gemm_quick_gelu_epilogue(dev, dtype, variant):
     """AACLIP_EPI_QGELU (towers built with quick_gelu=True) on every tile family, 16-bit
     and fp32 outputs, a ragged last M-tile; float64 reference. The fp32 kernel keeps
@@ -122,7 +123,7 @@ def test_gemm_gelu_flags_exclusive(dev):
                       torch.cuda.current_stream().cuda_stream)
 
 
-@pytest.mark.parametrize("variant", [3, 5])
+@pytest.mark.parametrize("variant", [3, 5, 10])
 @pytest.mark.parametrize("M,N,K", [(18464, 4096, 1024), (4100, 3072, 4096), (513, 256, 192), (9232, 1024, 4096)])
 def test_gemm_8phase_race_screen(dev, variant, M, N, K):
     """The 8-phase kernel's LDS hand-offs are placed by vmcnt/barrier counting: a read
@@ -146,6 +147,36 @@ def test_gemm_8phase_race_screen(dev, variant, M, N, K):
         _lib.call("aaclip_set_gemm_variant", 0)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(18464, 3072, 1024), (9232, 1024, 4096), (577 * 3, 1536, 1024), (300, 256, 192)])
+def test_gemm_families_bit_identical(dev, dt, M, N, K):
+    """Every 16-bit tile family accumulates the K dimension in the same order (32-element
+    MFMA k-slices, ascending, one fp32 accumulator per output), so their outputs are
+    bit-identical -- the engine may pick any family per shape, stream count and batch
+    without changing an image's bits. Covers the K-step-32 two-workgroup kernel against
+    the 8-phase, 320x256 and 128x128 ones (bf16 out with bias, fp32 out with residual)."""
+    g = torch.Generator(device=dev).manual_seed(M + K)
+    a = torch.randn(M, K, device=dev, generator=g).to(dt)
+    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
+    bias = torch.randn(N, device=dev, generator=g)
+    res = torch.randn(M, N, device=dev, generator=g)
+    fams = [f for f in (0, 3, 8, 9, 10) if N % 256 == 0 or f in (0, 9, 10)]
+    outs = []
+    for f in fams:
+        _lib.call("aaclip_set_gemm_variant", f)
+        try:
+            o16 = torch.empty(M, N, device=dev, dtype=dt)
+            ops.gemm(a, w, o16, bias=bias)
+            o32 = res.clone()
+            ops.gemm(a, w, o32, bias=bias, residual=o32)
+        finally:
+            _lib.call("aaclip_set_gemm_variant", 0)
+        outs.append((o16, o32))
+    for f, (o16, o32) in zip(fams[1:], outs[1:]):
+        assert torch.equal(o16.view(torch.int16), outs[0][0].view(torch.int16)), f
+        assert torch.equal(o32, outs[0][1]), f
+
+
 def test_gemm_bf16_asymmetric_identity(dev):
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     M = N = K = 256
@@ -156,7 +187,7 @@ def test_gemm_bf16_asymmetric_identity(dev):
     torch.testing.assert_close(out, w.float().T, atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 8, 9, 10])
 def test_gemm_epilogues_bf16(dev, variant):
     from aaclip import _lib
     _lib.call("aaclip_set_gemm_variant", variant)

@@ -1,0 +1,66 @@
+"""Whole two-stream C2 steps (B = 32, bf16, hipGraph) under GEMM tile-family arms, captured
+in ONE process and timed in interleaved rounds. An arm is `name=N:K:fam,N:K:fam,...`: the
+chunk's block-GEMM shape (rows = the chunk's B*577, N, K) pinned to tile family `fam`
+(aaclip_gemm_pin; pins are read at launch, so each capture keeps its own). Same bits in
+every arm (every family accumulates K in the same order) -- checked against arm 0.
+usage: python tools/step_arms.py base= outproj=1024:1024:10 nk1024=1024:1024:10,1024:4096:10"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "aa-clip_amd")]
+from aaclip import _lib  # noqa: E402
+from aaclip.engine import VisualEngine  # noqa: E402
+from bench import synthetic_visual_weights  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("arms", nargs="+")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--streams", type=int, default=2)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    vp, ad = synthetic_visual_weights(dev)
+    eng = VisualEngine(vp, ad, dtype=torch.bfloat16)
+    B, S = 32, 336
+    rows = (B // a.streams) * ((S // 14) ** 2 + 1)
+    g = torch.Generator(device=dev).manual_seed(111)
+    x = torch.randn(B, 3, S, S, device=dev, generator=g)
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
+    runs = {}
+    for arm in a.arms:
+        name, _, spec = arm.partition("=")
+        pins = [tuple(int(v) for v in p.split(":")) for p in spec.split(",") if p]
+        for n, k, fam in pins:
+            _lib.call("aaclip_gemm_pin", _lib.BF16, rows, n, k, fam)
+        runs[name] = eng.graphed_predict(B, S, "Industrial", streams=a.streams)  # dispatch baked in
+        for n, k, _ in pins:
+            _lib.call("aaclip_gemm_pin", _lib.BF16, rows, n, k, 0)
+    ref = None
+    for name, run in runs.items():
+        m, s = run(x, T)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = (m.clone(), s.clone())
+        print(f"{name}: bits {'same' if torch.equal(m, ref[0]) and torch.equal(s, ref[1]) else 'DIFF'}", flush=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(a.rounds):
+        for name, run in runs.items():
+            for _ in range(3):
+                run(x, T)
+            e0.record()
+            for _ in range(a.steps):
+                run(x, T)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / a.steps
+            print(f"round {r} {name}: {ms:.3f} ms/step  {B / ms * 1e3:.1f} img/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
