@@ -161,7 +161,10 @@ class VisualEngine:
         self.relu = r_det
         self.w_seg = [cdt(t) for t in self.w_seg[:-1]] + [cdt(torch.cat([self.w_seg[-1], w_det], 0))]
         self._ws = {}
-        self.map_fused = os.environ.get("AACLIP_MAP_FUSED", "1") != "0"
+        # the one-launch map (aaclip_anomaly_map_fused) is bit-identical but measured 115-119 us
+        # in-step vs 61 us for the two launches (agent-scope release/acquire per workgroup,
+        # 3 patch rows per wave: profiles/r03/map_fused_ab.txt): opt-in, AACLIP_MAP_FUSED=1
+        self.map_fused = os.environ.get("AACLIP_MAP_FUSED", "0") == "1"
         self.poison = False  # tests: fill new workspaces with NaN (read-before-write screen)
 
     # ------------------------------------------------------------------ workspace
@@ -373,8 +376,8 @@ class VisualEngine:
         pass of aaclip_anomaly_map_score (62.7 vs 65.1 us at B = 32, tools/map_ab.py), whose
         16-row workgroups stream at 4.6 TB/s where the one-row-per-wave map pass reaches
         6.4; the one-pass entry stays in the ABI, bit-identical (tests). The map itself is
-        one launch (aaclip_anomaly_map_fused: blur + upsample in the stream's tail) unless
-        AACLIP_MAP_FUSED=0 (the two-launch form, same bits)."""
+        two launches (patch scores, then blur + upsample); AACLIP_MAP_FUSED=1 selects the
+        one-launch aaclip_anomaly_map_fused (same bits, measured 2x slower in the step)."""
         if self.map_fused:
             ops.anomaly_map_fused(seg_raw, T, out_map, ws["grid"], ws["bandcnt"], g=ws["g"], ksize=k, sigma=s)
         else:
