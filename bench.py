@@ -745,7 +745,7 @@ def main():
         from aaclip import _lib
         _lib.call("aaclip_set_gemm_variant", args.gemm_variant)
         _lib.call("aaclip_set_attn_variant", args.attn_variant)
-    vp, ad = synthetic_visual_weights(dev)
+    vp, ad = synthetic_visual_weights(dev, n_tok=(args.img_size // 14) ** 2 + 1)
     eng = VisualEngine(vp, ad, dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16)
     B, S = args.batch, args.img_size
     # one global batch of B * world images (the same seeded tensor on every rank);
