@@ -528,6 +528,7 @@ class VisualEngine:
 
         run.graph = graph
         run.workspaces = held
+        run.slot0 = slot0  # the private workspace slots (tools / bench diagnostics re-capture on them)
         return run
 
 

@@ -155,6 +155,52 @@ def latency_b1(eng, size, T, reps=30):
     return {"batch": 1, "ms_per_image": round(ms, 3), "images_per_sec": round(1e3 / ms, 1)}
 
 
+def step_bounds(eng, run, x, T, streams, steps=10, rounds=2):
+    """Diagnostic (never `value`): what the GEMM epilogues cost in the timed step. The
+    shipped captured step vs the same step captured with every GEMM epilogue skipped
+    (aaclip_set_gemm_variant bit 9) or only its global stores skipped (bit 10), replayed on
+    the graph's own workspaces after a normal replay filled them with this batch's
+    activations (fresh zero buffers would let every later kernel multiply zeros and the chip
+    clock up). The skipped arms compute garbage; interleaved rounds, min per arm.
+    tools/epi_bound.py is the standalone form (profiles/r03/gemm_epilogue_bound.txt)."""
+    from aaclip import _lib
+    S = x.shape[-1]
+    slot0 = run.slot0  # `run`'s private workspace slots (graphed_predict)
+    graphs = {}
+    try:
+        for name, v in (("epilogue_skipped", 512), ("stores_skipped", 1024)):
+            _lib.call("aaclip_set_gemm_variant", v)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                eng.predict(x, T, "Industrial", streams=streams, _slot0=slot0)
+            graphs[name] = gr
+    finally:
+        _lib.call("aaclip_set_gemm_variant", 0)
+    arms = {"shipped": lambda: run(x, T)}
+    arms.update({k: g.replay for k, g in graphs.items()})
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = {}
+    for _ in range(rounds):
+        for name, fn in arms.items():
+            run(x, T)  # real activations in the workspaces before every arm
+            fn()
+            e0.record(st)
+            for _ in range(steps):
+                fn()
+            e1.record(st)
+            e1.synchronize()
+            best[name] = min(best.get(name, 1e9), e0.elapsed_time(e1) / steps)
+    run(x, T)
+    torch.cuda.synchronize()
+    base = best["shipped"]
+    return {"note": "diagnostic arms skip work (garbage outputs); never the timed value",
+            "ms_per_step": {k: round(v, 3) for k, v in best.items()},
+            "gemm_epilogue_ms": round(base - best["epilogue_skipped"], 3),
+            "gemm_epilogue_share": round((base - best["epilogue_skipped"]) / base, 3),
+            "gemm_store_ms": round(base - best["stores_skipped"], 3)}
+
+
 def preprocess_leg(dev, batch, size, reps=20):
     """SURVEY 8(f)-3 on device: B decoded uint8 RGB images (1024x1024, MVTec's size)
     -> Pillow-exact BICUBIC resize + ToTensor + Normalize -> fp32 [B,3,S,S]
@@ -851,6 +897,8 @@ def main():
         if args.isolated:
             line["isolated"] = {"gemm": roofline_gemm_isolated(eng, ws), "map": roofline_map_isolated(eng, ws, T)}
         line["latency_b1"] = latency_b1(eng, S, T)
+        if world == 1 and run is not None:
+            line["step_bounds"] = step_bounds(eng, run, x, T, args.streams)
     if rank == 0 and world == 1 and not args.no_modes:
         del run
         run = None

@@ -35,7 +35,7 @@ def main():
     for _ in range(3):
         run(x, T)  # the graph's workspaces now hold this batch's activations
     torch.cuda.synchronize()
-    slot0 = 1000 * eng._graphs  # graphed_predict's private workspace slots
+    slot0 = run.slot0  # graphed_predict's private workspace slots
     graphs = {}
     for v in [int(s) for s in a.variants.split(",")]:
         _lib.call("aaclip_set_gemm_variant", v)  # read at launch: baked into this capture
