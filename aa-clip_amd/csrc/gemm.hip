@@ -157,7 +157,7 @@ __device__ __forceinline__ void epilogue_store1(const GemmArgs& a, int m, int n,
 
 // Bijective XCD remap (blocks b, b+8, ... share an XCD) + grouped tile order.
 __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, int& tm, int& tn,
-                                            int GROUP_M = 8) {
+                                            int GROUP_M = 4) {
   const int nwg = tiles_m * tiles_n;
   const int xcd = bid & 7;
   const int q = nwg >> 3, r = nwg & 7;
@@ -1160,7 +1160,11 @@ bool prefer_8ph(int M, int N) {
   const int64_t c320 = ((t320 + cus - 1) / cus) * 320 * 11, c256 = ((t256 + cus - 1) / cus) * 256 * 10;
   return c256 < c320;
 }
-int g_group_m = 8;
+// Tile-order group height: 4 M-tiles per group, so an XCD's 32 co-resident tiles are 4 M x 8 N
+// -- each activation panel (streamed from HBM) feeds 8 tiles, each weight panel (shared by the
+// concurrent chunks, MALL-resident) 4. Two-stream C2 step +0.3-0.5 % over 8 (8 M x 4 N) in
+// 5 interleaved rounds (profiles/r03/gemm_group_height_ab.txt); 12 lost 1.2 %. Same bits.
+int g_group_m = 4;
 int g_setprio = 0;
 int g_dbg = 0;
 
@@ -1307,11 +1311,11 @@ extern "C" int aaclip_set_gemm_variant(int variant) {
   // 8-phase ping-pong everywhere / for N >= 2048, 5 = persistent 8-phase, 6 = MX fp8 on the
   // 256x256 LDS-DMA kernel instead
   // of its 8-phase default, 8 = 320x256 everywhere, 9 = 128x128, 10 = two-workgroup 256x128); bits 4-7: tile-order
-  // group height (0 = 8); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
+  // group height (0 = 4); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
   if (variant < 0 || variant >= 2048 || fam > 10 || fam == 7) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
-  g_group_m = grp ? grp : 8;
+  g_group_m = grp ? grp : 4;
   g_setprio = (variant >> 8) & 1;
   g_dbg = (variant >> 9) & 3;  // bit 9 skip epilogue, bit 10 skip the global stores
   return AACLIP_OK;

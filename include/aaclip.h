@@ -135,7 +135,7 @@ int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int
  * for N >= 2048 only, 8 = 320x256 everywhere, 9 = 128x128 everywhere, 10 = two
  * 4-wave 256x128 workgroups per CU (K-step 32; N % 128 == 0, K % 32 == 0); for the
  * fp8 MX GEMM: 0 = 8-phase ping-pong (default), 6 = the 256x256 LDS-DMA kernel; bits 4-7:
- * tile-order group height (0 = 8); bit 8: s_setprio around the MFMA cluster;
+ * tile-order group height (0 = 4); bit 8: s_setprio around the MFMA cluster;
  * bit 9: diagnostic timing mode that skips the epilogue (outputs NOT written);
  * bit 10: diagnostic mode that runs the epilogue but skips its global stores.
  * Process-global; not for production use.

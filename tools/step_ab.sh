@@ -2,7 +2,7 @@
 # usage (GPU box): bash tools/step_ab.sh "--attn-variant 1" "--attn-variant 3" "--streams 3"
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-for r in 1 2; do
+for r in ${ROUNDS:-1 2}; do
   i=0
   for flags in "$@"; do
     timeout -k 10 120 python bench.py --steps 30 --warmup 3 --no-roofline --cpu-seconds 0 --no-modes --no-c5 \
