@@ -343,7 +343,7 @@ def im2col(img: torch.Tensor, cols: torch.Tensor, patch: int) -> torch.Tensor:
         raise ValueError("image must be contiguous fp32 [B,C,S,S]")
     if cols.shape[0] != B * g * g or not cols.is_contiguous():
         raise ValueError("cols shape mismatch")
-    _launch("im2col", "im2col_kernel", 0.0, img.numel() * 4 + cols.numel() * cols.element_size(), "aaclip_im2col",
+    _launch("im2col", "im2col_band_kernel", 0.0, img.numel() * 4 + cols.numel() * cols.element_size(), "aaclip_im2col",
             dtag(cols), _ptr(img), _ptr(cols), B, C, S, patch, cols.shape[1], _stream())
     return cols
 

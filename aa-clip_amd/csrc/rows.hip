@@ -326,6 +326,51 @@ __global__ __launch_bounds__(256) void anchor_reduce_kernel(const float* emb, in
   for (int j = threadIdx.x; j < dim; j += 256, ++cnt) T[(size_t)j * ncols + col] = m_local[cnt] * inv;
 }
 
+// One workgroup per (image, patch row, channel): the P image rows a patch row spans
+// are P*S contiguous floats, read with full-width loads into LDS; each of the g
+// patches then writes this channel's P*P values as one contiguous run of its cols row
+// (two k per lane-store), and the last channel's workgroup zero-fills k >= C*P*P.
+// Both sides coalesced (the per-thread 8-k form reads 2 scattered 32-B runs per
+// thread). Pure copy + the same conversions: the same bits as im2col_kernel.
+__global__ __launch_bounds__(256) void im2col_band_kernel(int out_dtype, const float* img, void* cols, int C,
+                                                          int S, int P, int g, int kp) {
+  extern __shared__ __attribute__((aligned(16))) float band[];  // [P][S]
+  const int c = blockIdx.x % C;
+  const int bp = blockIdx.x / C;
+  const int py = bp % g, b = bp / g;
+  const float* src = img + (((size_t)b * C + c) * S + (size_t)py * P) * S;
+  const int n = P * S;
+  if ((S & 3) == 0 && ((uintptr_t)img & 15) == 0) {
+    for (int i = threadIdx.x; i < n / 4; i += 256) ((float4_t*)band)[i] = ((const float4_t*)src)[i];
+  } else {
+    for (int i = threadIdx.x; i < n; i += 256) band[i] = src[i];
+  }
+  __syncthreads();
+  const int pp = P * P;
+  const int kreal = C * pp;
+  const int k0 = c * pp;
+  const int kend = c == C - 1 ? kp : k0 + pp;  // the last channel also writes the zero pad
+  const int npair = (kend - k0) / 2;          // pp, kreal and kp are even
+  const size_t row0 = ((size_t)b * g + py) * g;
+  for (int i = threadIdx.x; i < g * npair; i += 256) {
+    const int px = i / npair;
+    const int k = k0 + 2 * (i % npair);
+    float v[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kk = k + j - k0;
+      v[j] = k + j < kreal ? band[(kk / P) * S + px * P + kk % P] : 0.f;
+    }
+    const size_t o = (row0 + px) * kp + k;
+    if (out_dtype == AACLIP_F32)
+      *(float2_t*)((float*)cols + o) = float2_t{v[0], v[1]};
+    else if (out_dtype == AACLIP_F16)
+      *(uint32_t*)((uint16_t*)cols + o) = pack_f16x2(v[0], v[1]);
+    else
+      *(uint32_t*)((uint16_t*)cols + o) = pack_bf16x2(v[0], v[1]);
+  }
+}
+
 // 8 consecutive k of one patch row per thread.
 __global__ __launch_bounds__(256) void im2col_kernel(int out_dtype, const float* img, void* cols,
                                                      int batch, int C, int S, int P, int g,
@@ -565,9 +610,15 @@ extern "C" int aaclip_im2col(int out_dtype, const float* img, void* cols, int ba
   AACLIP_REQUIRE(dtype_ok(out_dtype) && img && cols && batch > 0 && channels > 0 && patch > 0);
   AACLIP_REQUIRE(img_size % patch == 0 && k_padded % 8 == 0 && k_padded >= channels * patch * patch);
   const int g = img_size / patch;
-  const size_t total = (size_t)batch * g * g * (k_padded / 8);
-  im2col_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      out_dtype, img, cols, batch, channels, img_size, patch, g, k_padded);
+  const size_t band_bytes = (size_t)patch * img_size * sizeof(float);
+  if (band_bytes <= 65536 && patch % 2 == 0) {  // every ViT-L/14 size (14 x 518 x 4 = 29 KB)
+    im2col_band_kernel<<<(unsigned)(batch * g * channels), 256, band_bytes, (hipStream_t)stream>>>(
+        out_dtype, img, cols, channels, img_size, patch, g, k_padded);
+  } else {
+    const size_t total = (size_t)batch * g * g * (k_padded / 8);
+    im2col_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        out_dtype, img, cols, batch, channels, img_size, patch, g, k_padded);
+  }
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

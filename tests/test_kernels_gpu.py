@@ -466,6 +466,26 @@ def test_block_tail_and_embed(dev):
     np.testing.assert_allclose(tap.cpu().numpy(), tr, atol=1e-4, rtol=1e-4)
 
 
+# ----------------------------------------------------------------------------- im2col
+@pytest.mark.parametrize("S", [336, 448, 518, 28])
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.bfloat16])
+def test_im2col_exact(dev, S, dt):
+    """aaclip_im2col (conv1 as a GEMM, model/adapter.py:68): cols[b*g*g + p, c*196 + kh*14 + kw]
+    = img[b, c, 14*py + kh, 14*px + kw] cast to the cols dtype, zero for k >= 588 -- bit-exact
+    against torch's unfold, including a misaligned (offset) image view."""
+    torch.manual_seed(S)
+    B, C, P, kp = 3, 3, 14, 640
+    base = torch.randn(B * C * S * S + 1, device=dev)
+    for img in (base[:-1].view(B, C, S, S), base[1:].view(B, C, S, S)):
+        g = S // P
+        cols = torch.full((B * g * g, kp), float("nan"), device=dev, dtype=dt)
+        ops.im2col(img, cols, P)
+        ref = torch.nn.functional.unfold(img, P, stride=P).transpose(1, 2).reshape(B * g * g, C * P * P)
+        torch.cuda.synchronize()
+        assert torch.equal(cols[:, :C * P * P], ref.to(dt))
+        assert torch.equal(cols[:, C * P * P:], torch.zeros_like(cols[:, C * P * P:]))
+
+
 # ----------------------------------------------------------------------------- anomaly map
 @pytest.mark.parametrize("dom", ["Industrial", "Medical"])
 def test_similarity_map_golden(dev, golden, dom):
