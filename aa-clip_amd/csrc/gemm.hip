@@ -1153,6 +1153,13 @@ bool prefer_small(int M, int N, bool ph8) {
   return 2 * tiles < cu_count();
 }
 
+// Single images (M = 577): when even 128x128 tiles number fewer than half the CUs
+// (batch-1 QKV 120, out-proj / c_proj / adapters 40), 64x64 tiles (4 waves of 32x32)
+// give 4x the workgroups; same K order, same bits.
+bool prefer_tiny(int M, int N) {
+  return N % 64 == 0 && 2 * (int64_t)ceil_div(M, 128) * (N / 128) < cu_count();
+}
+
 // tile rounds x tile rows, 8-phase 256-row tiles weighted 10/11 for their faster main loop
 bool prefer_8ph(int M, int N) {
   const int cus = cu_count();
@@ -1199,7 +1206,7 @@ int pinned_family(int dtype, int M, int N, int K) {
 thread_local int t_concurrent = 0;
 
 enum Kern { KERN_256x256 = 1, KERN_256x128 = 2, KERN_8PH = 3, KERN_8PH_PERSIST = 5, KERN_320x256 = 8,
-            KERN_128x128 = 9, KERN_PP2 = 10 };
+            KERN_128x128 = 9, KERN_PP2 = 10, KERN_64x64 = 11 };
 
 // The kernel a 16-bit GEMM of this shape launches: the A/B variant hook, else a pin,
 // else the concurrent-chunk rule, else the per-shape heuristic (fewer tile rounds
@@ -1223,6 +1230,9 @@ int choose16(int dtype, int M, int N, int K, bool fits) {
       if (N % 256 == 0 && fits) return KERN_8PH_PERSIST;
       break;
     case 9: return KERN_128x128;  // 128x128 everywhere (A/B)
+    case 11:  // 64x64 everywhere (A/B)
+      if (N % 64 == 0) return KERN_64x64;
+      break;
     case 10:  // two workgroups per CU, 256x128 tile, K-step 32
       if (fits && K % 32 == 0) return KERN_PP2;
       break;
@@ -1233,7 +1243,7 @@ int choose16(int dtype, int M, int N, int K, bool fits) {
   }
   if (N % 256 == 0 && fam == 0) {
     const bool ph8 = fits && prefer_8ph(M, N);
-    if (prefer_small(M, N, ph8)) return KERN_128x128;
+    if (prefer_small(M, N, ph8)) return prefer_tiny(M, N) ? KERN_64x64 : KERN_128x128;
     if (ph8) return KERN_8PH;
   }
   return N % 256 == 0 ? KERN_320x256 : KERN_256x128;
@@ -1251,6 +1261,7 @@ int dispatch16(GemmArgs a, hipStream_t s) {
     case KERN_8PH_PERSIST: return launch_bf16_8ph<H16, true>(a, s);
     case KERN_320x256: return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
     case KERN_128x128: return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);
+    case KERN_64x64: return launch_bf16<64, 64, 2, 2, 0, H16>(a, s);
     case KERN_PP2: return launch_bf16_pp2<H16>(a, s);
     default: return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
   }
@@ -1270,6 +1281,7 @@ extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
     case KERN_8PH_PERSIST: return "gemm_bf16_8ph_kernel<256,256,persistent>";
     case KERN_320x256: return "gemm_bf16_kernel<320,256,2,4>";
     case KERN_128x128: return "gemm_bf16_kernel<128,128,2,2>";
+    case KERN_64x64: return "gemm_bf16_kernel<64,64,2,2>";
     case KERN_PP2: return "gemm_bf16_pp2_kernel<256,128>";
     default: return "gemm_bf16_kernel<256,128,4,2>";
   }
@@ -1278,8 +1290,8 @@ extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
 extern "C" int aaclip_gemm_pin(int in_dtype, int M, int N, int K, int family) {
   AACLIP_REQUIRE((in_dtype == AACLIP_BF16 || in_dtype == AACLIP_F16) && M > 0 && N > 0 && K > 0);
   AACLIP_REQUIRE(family == 0 || family == 1 || family == 2 || family == 3 || family == 8 || family == 9 ||
-                 family == 10);
-  AACLIP_REQUIRE(family == 0 || family == 2 || family == 10 || N % 256 == 0);
+                 family == 10 || family == 11);
+  AACLIP_REQUIRE(family == 0 || family == 2 || family == 10 || family == 11 || N % 256 == 0);
   std::lock_guard<std::mutex> lk(g_pin_mu);
   const int n = g_npins.load(std::memory_order_relaxed);
   for (int i = 0; i < n; ++i)
@@ -1310,10 +1322,11 @@ extern "C" int aaclip_set_gemm_variant(int variant) {
   // bits 0-3: tile family (0 default = per-shape choice, 1 = 256x256, 2 = 256x128, 3/4 = 256x256
   // 8-phase ping-pong everywhere / for N >= 2048, 5 = persistent 8-phase, 6 = MX fp8 on the
   // 256x256 LDS-DMA kernel instead
-  // of its 8-phase default, 8 = 320x256 everywhere, 9 = 128x128, 10 = two-workgroup 256x128); bits 4-7: tile-order
+  // of its 8-phase default, 8 = 320x256 everywhere, 9 = 128x128, 10 = two-workgroup 256x128,
+  // 11 = 64x64); bits 4-7: tile-order
   // group height (0 = 4); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 2048 || fam > 10 || fam == 7) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 2048 || fam > 11 || fam == 7) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 4;
   g_setprio = (variant >> 8) & 1;

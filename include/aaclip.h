@@ -133,7 +133,8 @@ int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int
  * and 128x128 when that choice would fill under half the CUs; else 256x128),
  * 1 = 256x256 (N % 256 == 0), 2 = 256x128, 3 = 8-phase everywhere, 4 = 8-phase
  * for N >= 2048 only, 8 = 320x256 everywhere, 9 = 128x128 everywhere, 10 = two
- * 4-wave 256x128 workgroups per CU (K-step 32; N % 128 == 0, K % 32 == 0); for the
+ * 4-wave 256x128 workgroups per CU (K-step 32; N % 128 == 0, K % 32 == 0), 11 = 64x64
+ * everywhere (N % 64 == 0; the default for single-image shapes); for the
  * fp8 MX GEMM: 0 = 8-phase ping-pong (default), 6 = the 256x256 LDS-DMA kernel; bits 4-7:
  * tile-order group height (0 = 4); bit 8: s_setprio around the MFMA cluster;
  * bit 9: diagnostic timing mode that skips the epilogue (outputs NOT written);
@@ -145,7 +146,7 @@ int aaclip_set_gemm_variant(int variant);
 /*
  * Pin the tile family aaclip_gemm uses for one (in_dtype, M, N, K) (bf16 / f16):
  * 1 = 256x256, 2 = 256x128, 3 = 256x256 8-phase ping-pong, 8 = 320x256,
- * 9 = 128x128, 10 = two 4-wave 256x128 workgroups per CU, 0 = unpin (back to the
+ * 9 = 128x128, 10 = two 4-wave 256x128 workgroups per CU, 11 = 64x64, 0 = unpin (back to the
  * heuristic). Set by a measuring tuner at
  * engine setup (aaclip/ops.py tune_gemm); every family accumulates K in the same
  * order, so a pin changes speed, never bits. Process-global (mutex-guarded), host

@@ -13,7 +13,7 @@ from aaclip import _lib, ops
 
 pytestmark = pytest.mark.gpu
 
-FAMILIES = (0, 1, 2, 3, 5, 8, 9)  # default dispatch + every forced tile family
+FAMILIES = (0, 1, 2, 3, 5, 8, 9, 11)  # default dispatch + every forced tile family
 
 
 def _gemm_case(seed):

@@ -148,19 +148,20 @@ def test_gemm_8phase_race_screen(dev, variant, M, N, K):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("M,N,K", [(18464, 3072, 1024), (9232, 1024, 4096), (577 * 3, 1536, 1024), (300, 256, 192)])
+@pytest.mark.parametrize("M,N,K", [(18464, 3072, 1024), (9232, 1024, 4096), (577 * 3, 1536, 1024), (300, 256, 192),
+                                   (577, 1024, 4096), (577, 768, 1024)])
 def test_gemm_families_bit_identical(dev, dt, M, N, K):
     """Every 16-bit tile family accumulates the K dimension in the same order (32-element
     MFMA k-slices, ascending, one fp32 accumulator per output), so their outputs are
     bit-identical -- the engine may pick any family per shape, stream count and batch
     without changing an image's bits. Covers the K-step-32 two-workgroup kernel against
-    the 8-phase, 320x256 and 128x128 ones (bf16 out with bias, fp32 out with residual)."""
+    the 8-phase, 320x256, 128x128 and 64x64 ones (bf16 out with bias, fp32 out with residual)."""
     g = torch.Generator(device=dev).manual_seed(M + K)
     a = torch.randn(M, K, device=dev, generator=g).to(dt)
     w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
     bias = torch.randn(N, device=dev, generator=g)
     res = torch.randn(M, N, device=dev, generator=g)
-    fams = [f for f in (0, 3, 8, 9, 10) if N % 256 == 0 or f in (0, 9, 10)]
+    fams = [f for f in (0, 3, 8, 9, 10, 11) if N % 256 == 0 or f in (0, 9, 10, 11)]
     outs = []
     for f in fams:
         _lib.call("aaclip_set_gemm_variant", f)
