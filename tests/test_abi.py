@@ -75,8 +75,11 @@ def test_gemm_plan_per_shape_choice():
     # whole-batch launches (bench roofline shapes)
     assert [plan(18464, n) for n in (3072, 1024, 4096)] == [ph8, t320, ph8]
     # a few images: 128x128 tiles when the big-tile choice fills under half the CUs
-    small = "gemm_bf16_kernel<128,128,2,2>"
-    assert [plan(577, n) for n in (3072, 1024, 4096)] == [small] * 3
+    small, tiny = "gemm_bf16_kernel<128,128,2,2>", "gemm_bf16_kernel<64,64,2,2>"
+    # one image: 64x64 tiles where even 128x128 ones number under half the CUs (QKV 120,
+    # out-proj / c_proj 40 tiles), 128x128 for c_fc (160)
+    assert [plan(577, n) for n in (3072, 1024, 4096)] == [tiny, tiny, small]
+    assert plan(577, 1024, 4096) == tiny  # c_proj
     assert [plan(4616, n) for n in (3072, 1024, 4096)] == [ph8, small, t320]
     assert plan(100, 384) == "gemm_bf16_kernel<256,128,4,2>"
     assert lib.aaclip_gemm_plan(_lib.F32, 100, 256, 64) == b"gemm_f32_kernel"
