@@ -49,6 +49,7 @@ SIGNATURES = {
     "aaclip_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],
     "aaclip_block_tail": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],
     "aaclip_layernorm": [_I, _P, _L, _P, _P, _P, _L, _I, _I, _P, _L, _P],
+    "aaclip_residual_layernorm": [_I, _P, _P, _P, _P, _P, _I, _I, _P, _L, _P],
     "aaclip_text_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "aaclip_eot_ln": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "aaclip_anchor_reduce": [_P, _I, _I, _P, _I, _I, _P],

@@ -166,6 +166,10 @@ class VisualEngine:
         # 3 patch rows per wave: profiles/r03/map_fused_ab.txt): opt-in, AACLIP_MAP_FUSED=1
         self.map_fused = os.environ.get("AACLIP_MAP_FUSED", "0") == "1"
         self.poison = False  # tests: fill new workspaces with NaN (read-before-write screen)
+        # deferred out-proj residual (A/B, AACLIP_DEFER_RESID=1): out-proj writes acc + bias to
+        # the u workspace with no residual read, and ln_2 does x += d before normalising
+        # (aaclip_residual_layernorm; the same fp32 add, bit-identical)
+        self.defer_resid = os.environ.get("AACLIP_DEFER_RESID", "0") == "1"
 
     # ------------------------------------------------------------------ workspace
     def _workspace(self, B: int, S: int, slot: int = 0):
@@ -300,19 +304,30 @@ class VisualEngine:
             def attend():
                 ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS, q_prescaled=self.q_prescaled)
 
+            defer = self.defer_resid
+
             def out_proj(blk):
-                ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
+                if defer:  # acc + bias only; ln_2 adds it to x (ln2 below)
+                    ops.gemm(ws["attn"], blk["w_o"], ws["u"], bias=blk["b_o"])
+                else:
+                    ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
+
+            def ln2(blk, y, y_sc=None):
+                if defer:
+                    ops.residual_layernorm(X, ws["u"], blk["ln2"][0], blk["ln2"][1], y, y_sc=y_sc)
+                else:
+                    ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], y, y_sc=y_sc)
 
             def mlp(blk, aux):
                 if self.fp8_mlp_only:  # ln_2 -> MX e4m3 -> c_fc (fp8, GELU, MX out) -> c_proj (fp8)
                     a8, asc, f8, fsc = ws["a8"], ws["asc"], ws["f8"], ws["fsc"]
-                    ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], a8, y_sc=asc)
+                    ln2(blk, a8, y_sc=asc)
                     ops.gemm_fp8mx(a8, asc, blk["w_fc"][0], blk["w_fc"][1], f8, out_sc=fsc, bias=blk["b_fc"],
                                    gelu=self.act)
                     ops.gemm_fp8mx(f8, fsc, blk["w_pr"][0], blk["w_pr"][1], X, bias=blk["b_pr"], residual=X,
                                    aux=aux)
                     return
-                ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], H)
+                ln2(blk, H)
                 ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=self.act)
                 ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=aux)
         for i in range(last):
@@ -468,26 +483,31 @@ class VisualEngine:
             main.wait_event(ev)
         return out_map, out_score
 
-    GRAPH_CACHE = 4  # captured steps kept per engine (predict_cached)
+    GRAPH_CACHE = 4  # captured steps kept per engine (predict_cached), least recently used dropped
 
     def predict_cached(self, x: torch.Tensor, T: torch.Tensor, domain: str = "Industrial", streams=1):
         """predict() through a captured hipGraph once a (batch, size, domain, streams) shape
-        repeats (the harness's full batches): the first call of a shape runs eagerly, the
-        second captures, later ones replay (inputs copied into the graph's static
-        buffers). Same kernels, same bits (tests/test_e2e_gpu.py); the outputs are
+        repeats BACK TO BACK (the harness's full batches within a class, or one-batch
+        classes of equal size): a shape runs eagerly until it follows a call of the same
+        shape, then that call captures and later ones replay (inputs copied into the
+        graph's static buffers). A class's tail batch is followed by another shape, so it
+        never triggers a capture (no warm-up + capture + device sync for a shape that is
+        not coming back) and never evicts a full-batch graph; eviction is least recently
+        used. Same kernels, same bits (tests/test_e2e_gpu.py); the outputs are
         graph-owned buffers, overwritten by the next replay of that shape."""
         key = (x.shape[0], x.shape[-1], domain, tuple(streams) if isinstance(streams, (tuple, list)) else streams)
         if not hasattr(self, "_graph_cache"):
-            self._graph_cache, self._seen = {}, {}
+            self._graph_cache, self._last_key = {}, None
         run = self._graph_cache.get(key)
+        repeat, self._last_key = key == self._last_key, key
         if run is None:
-            self._seen[key] = self._seen.get(key, 0) + 1
-            if self._seen[key] < 2 or not x.is_cuda:
+            if not repeat or not x.is_cuda:
                 return self.predict(x, T, domain, streams=streams)
             if len(self._graph_cache) >= self.GRAPH_CACHE:
-                self._graph_cache.pop(next(iter(self._graph_cache)))
+                self._graph_cache.pop(next(iter(self._graph_cache)))  # the least recently used
             run = self.graphed_predict(x.shape[0], x.shape[-1], domain, streams=streams)
-            self._graph_cache[key] = run
+        self._graph_cache.pop(key, None)
+        self._graph_cache[key] = run  # most recently used last
         return run(x, T.to(self.device, torch.float32))
 
     @torch.no_grad()
@@ -514,7 +534,11 @@ class VisualEngine:
         torch.cuda.synchronize(self.device)
         mine = {k: v for k, v in self._ws.items() if k not in before}  # the graph's own workspaces
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread_local: only this thread's calls are checked against the capture. The harness
+        # captures while its DataLoader's pin-memory thread keeps allocating pinned host
+        # buffers and querying events; "global" mode would fail the capture (or that
+        # thread) for calls that never touch the captured streams
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             out_map, out_score = self.predict(x_s, T_s, domain, streams=streams, _slot0=slot0)
         held = list(mine.values())  # kept alive by the graph even if the LRU drops their keys
         dev = self.device

@@ -113,9 +113,20 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
 
 
 # tile families aaclip_gemm_pin accepts (include/aaclip.h): 8-phase 256x256, 320x256,
-# 256x256, 128x128, 256x128
-GEMM_FAMILIES = (3, 8, 1, 9, 2)
+# 256x256, 128x128, 256x128, two-workgroup 256x128, 64x64
+GEMM_FAMILIES = (3, 8, 1, 9, 2, 10, 11)
 _tuned = {}
+
+
+def _family_applies(fam: int, N: int, K: int) -> bool:
+    """The shapes aaclip_gemm_pin / choose16 honour a family on (else it falls back)."""
+    if fam in (1, 3, 8, 9):
+        return N % 256 == 0
+    if fam == 10:
+        return K % 32 == 0
+    if fam == 11:
+        return N % 64 == 0
+    return True  # 0 (the unpinned per-shape heuristic) and 2
 
 
 def pin_gemm(dtype: int, M: int, N: int, K: int, family: int) -> None:
@@ -163,8 +174,10 @@ def tune_gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, reps: int = 3
     st = torch.cuda.current_stream()
     best, best_t = 0, float("inf")
     try:
-        for fam in GEMM_FAMILIES:
-            if fam != 2 and N % 256:
+        # family 0 = unpinned: the heuristic's own choice (e.g. the 64x64 tiles it takes for
+        # single-image shapes) is a candidate, so a pin is never slower than no pin
+        for fam in (0,) + GEMM_FAMILIES:
+            if not _family_applies(fam, N, K):
                 continue
             call("aaclip_gemm_pin", key[0], M, N, K, fam)
             gemm(a, w, out, **epilogue)
@@ -401,6 +414,23 @@ def layernorm(x, w, b, y, y_sc=None):
     _launch("layernorm", "layernorm_kernel", 0.0, x.numel() * 4 + y.numel() * y.element_size(), "aaclip_layernorm",
             od, _ptr(x), x.stride(0), _ptr(w), _ptr(b), _ptr(y), y.stride(0), x.shape[0], x.shape[1], scp, ld,
             _stream())
+    return y
+
+
+def residual_layernorm(x, d, w, b, y, y_sc=None):
+    """x += d (in place, fp32: the deferred out-proj residual add), then y = LN(x)
+    (aaclip_residual_layernorm). Bit-identical to gemm(..., residual=x) + layernorm."""
+    _dev(x, d, y)
+    for t, n in ((x, "x"), (d, "d"), (y, "y")):
+        _rowmajor(t, n)
+    if x.shape != y.shape or x.shape != d.shape or x.dtype != torch.float32 or d.dtype != torch.float32:
+        raise ValueError("residual_layernorm shape/dtype mismatch")
+    if not (x.is_contiguous() and d.is_contiguous() and (y.is_contiguous() or y_sc is not None)):
+        raise ValueError("residual_layernorm needs contiguous rows")
+    od, scp, ld = _mx_out(y, y_sc, x.shape[0])
+    _launch("residual_layernorm", "residual_ln_kernel", 0.0, x.numel() * 12 + y.numel() * y.element_size(),
+            "aaclip_residual_layernorm", od, _ptr(x), _ptr(d), _ptr(w), _ptr(b), _ptr(y), x.shape[0], x.shape[1],
+            scp, ld, _stream())
     return y
 
 

@@ -583,6 +583,22 @@ extern "C" int aaclip_patch_logits(int in_dtype, const void* f, int64_t ld, cons
   return AACLIP_OK;
 }
 
+// LDS bytes stage 2 needs for C channels: the source rows a band's taps can reach.
+static size_t blur_upsample_lds(int C, int g, int S, int ksize) {
+  const float scale = (float)(g - 1) / (float)(S - 1);
+  const int span = (int)(scale * (float)(kBand - 1)) + 4;  // source rows a band's taps can reach (+1 margin)
+  const int brows = min(g, span);
+  const int xrows = min(g, brows + 2 * (ksize / 2));
+  return (size_t)C * (2 * xrows + brows) * g * sizeof(float);
+}
+
+// Every argument check of aaclip_blur_upsample, so the multi-launch entry points can
+// reject a bad call before their first launch (no half-written map on an error).
+static bool blur_upsample_args_ok(int channels, int g, int out_size, int ksize) {
+  return channels >= 1 && channels <= kMaxC && g >= 2 && g <= 64 && out_size >= 2 && ksize >= 0 && ksize <= 15 &&
+         (ksize == 0 || (ksize % 2 == 1 && ksize / 2 < g)) && blur_upsample_lds(channels, g, out_size, ksize) <= 64 * 1024;
+}
+
 // Launch stage 2 for (C, ksize): rows of LDS the band needs, sized on the host.
 template <int C>
 int launch_blur_upsample(const float* grid, float* out, int batch, int g, int S, int ksize, const Gauss& gw,
@@ -590,7 +606,7 @@ int launch_blur_upsample(const float* grid, float* out, int batch, int g, int S,
   const int span = (int)(scale * (float)(kBand - 1)) + 4;  // source rows a band's taps can reach (+1 margin)
   const int brows = min(g, span);
   const int xrows = min(g, brows + 2 * (ksize / 2));
-  const size_t lds = (size_t)C * (2 * xrows + brows) * g * sizeof(float);
+  const size_t lds = blur_upsample_lds(C, g, S, ksize);
   if (lds > 64 * 1024) return AACLIP_ERR_ARG;
   const dim3 grd(ceil_div(S, kBand), batch);
 #define BU_LAUNCH(K) \
@@ -606,9 +622,8 @@ int launch_blur_upsample(const float* grid, float* out, int batch, int g, int S,
 extern "C" int aaclip_blur_upsample(const float* grid, float* out, int batch, int channels, int g,
                                     int out_size, int ksize, float sigma, int softmax,
                                     void* stream) {
-  AACLIP_REQUIRE(grid && out && batch > 0 && channels >= 1 && channels <= kMaxC);
-  AACLIP_REQUIRE(g >= 2 && g <= 64 && out_size >= 2);
-  AACLIP_REQUIRE(ksize >= 0 && ksize <= 15 && (ksize == 0 || (ksize % 2 == 1 && ksize / 2 < g)));
+  AACLIP_REQUIRE(grid && out && batch > 0);
+  AACLIP_REQUIRE(blur_upsample_args_ok(channels, g, out_size, ksize));
   const Gauss gw = ksize > 0 ? gaussian_weights(ksize, sigma) : Gauss{};
   const float scale = (float)(g - 1) / (float)(out_size - 1);
   hipStream_t s = (hipStream_t)stream;
@@ -632,7 +647,8 @@ extern "C" int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n
                                   const float* T, int batch, int g, int channels, int normalize,
                                   int out_size, int ksize, float sigma, float* grid_ws,
                                   float* out, void* stream) {
-  AACLIP_REQUIRE(grid_ws && batch > 0);
+  AACLIP_REQUIRE(grid_ws && out && batch > 0);
+  AACLIP_REQUIRE(blur_upsample_args_ok(1, g, out_size, ksize));  // before the first launch
   int rc = aaclip_patch_scores(in_dtype, levels, n_levels, ld, T, batch * g * g, channels,
                                normalize, 0, 0, grid_ws, stream);
   if (rc) return rc;
@@ -715,6 +731,7 @@ extern "C" int aaclip_anomaly_map_score(int in_dtype, const void* const* levels,
   AACLIP_REQUIRE(levels && det_raw && T && grid_ws && partial && out && score && batch > 0 && g >= 2);
   AACLIP_REQUIRE(channels == 768 && ld >= channels && ld % 4 == 0);
   AACLIP_REQUIRE(n_levels >= 1 && n_levels <= kMaxLevels);
+  AACLIP_REQUIRE(blur_upsample_args_ok(1, g, out_size, ksize));  // before map_det_kernel writes anything
   LevelPtrs lv{};
   for (int i = 0; i < n_levels; ++i) {
     AACLIP_REQUIRE(levels[i] != nullptr);

@@ -497,6 +497,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   EPI_CASE(1, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)                     // c_fc, quick_gelu towers
   EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)                     // out-proj, c_proj
   EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)  // c_proj + bf16 copy
+  EPI_CASE(0, AACLIP_EPI_BIAS)                                        // out-proj, deferred residual
   EPI_CASE(0, AACLIP_EPI_LEAKY)                                       // adapters, seg/det proj
   EPI_CASE(0, 0)                                                      // seg/det proj (no relu)
   EPI_CASE(0, EPI_REMAP)                                              // patch embedding
@@ -773,6 +774,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU, RM * RN / 2)
       EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID, RM * RN)
       EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16, RM * RN + RM * RN / 2)
+      EPI_CASE(false, AACLIP_EPI_BIAS, RM * RN)  // out-proj, deferred residual
       EPI_CASE(false, AACLIP_EPI_LEAKY, RM * RN)
 #undef EPI_CASE
       if (bf16_out)
@@ -1066,6 +1068,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_pp2_kernel(GemmArgs a) {
   EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)
   EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)
   EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)
+  EPI_CASE(false, AACLIP_EPI_BIAS)
   EPI_CASE(false, AACLIP_EPI_LEAKY)
 #undef EPI_CASE
   if (bf16_out)

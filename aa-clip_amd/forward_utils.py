@@ -12,7 +12,7 @@
   metrics_eval               forward_utils.py:233-280 — on device (aaclip_metrics_eval:
       min-max normalisation, score fusion, radix-sorted exact tie-aware AUROC / AP,
       identical to sklearn after the reference's 4-decimal rounding). numpy inputs
-      on a host without a GPU use the reference's own numpy/sklearn formulation.
+      are copied to the device; there is no CPU path (without a GPU it raises).
 Training losses and visualize() (cv2) are out of scope.
 """
 from __future__ import annotations

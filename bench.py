@@ -14,7 +14,9 @@ synthetic (no checkpoint in the image), bf16 compute.
 Prints ONE JSON line on rank 0 (contract in the task statement), with a
 `roofline` object for the dominant kernel (bf16 GEMM, MFMA-bound), a
 `roofline_map` object for the anomaly-map stream kernel (HBM-bound) and a
-`cpu_baseline` measured with the numpy oracle on this host's cores.
+`cpu_baseline` measured with the torch-CPU oracle (oracle/aaclip_torch.py: the
+reference's fp32 arithmetic on ATen's CPU kernels, calibrated against the
+reference itself) on this host's cores.
 """
 from __future__ import annotations
 
@@ -702,7 +704,11 @@ def _parity_size(dev, streams, S, sd, ia, x, T, refs, synth):
         err = np.abs(gpu_maps - ref_maps)
         flips = grid.argmax(-1) != ref_grid.argmax(-1)
         auc_gpu = float(roc_auc_score(lab, gpu_maps.reshape(-1)))
+        # per level (grid axis 1): a kernel change that doubles one level's flips shows here
+        per_level = [int(flips[:, lv][sure[:, lv]].sum()) for lv in range(flips.shape[1])]
         out[tag] = {"patch_label_flips_sure": int(flips[sure].sum()), "patch_label_flips_all": int(flips.sum()),
+                    "patch_label_flips_sure_per_level": per_level,
+                    "patch_label_flip_rate_sure": round(float(flips[sure].mean()), 6),
                     "anchor_logit_max_abs_err": float(np.abs(grid - ref_grid).max()),
                     "pixel_auroc_gpu": round(auc_gpu, 6), "pixel_auroc_abs_diff": abs(auc_gpu - auc_cpu),
                     "map_max_abs_err": float(err.max()), "map_within_tol": bool((err <= tol).all()),

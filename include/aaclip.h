@@ -239,6 +239,18 @@ int aaclip_layernorm(int out_dtype, const float* x, int64_t ldx, const float* w,
                      void* y_mx, int64_t ld_mx, void* stream);
 
 /*
+ * Deferred residual add + LN: x[row] = x[row] + d[row] (fp32, in place); y = LN(x).
+ * With d = the out-proj GEMM's (acc + bias) written without a residual read, this is
+ * the same fp32 add the GEMM epilogue's AACLIP_EPI_RESID performs (the add commutes),
+ * so x and y are bit-identical to out-proj(+resid) followed by aaclip_layernorm.
+ * x, d: [rows, width] fp32 contiguous; y as aaclip_layernorm (ldy = width).
+ * Replaces: the residual add of transformer.py:256 + ln_2 of transformer.py:257.
+ */
+int aaclip_residual_layernorm(int out_dtype, float* x, const float* d, const float* w,
+                              const float* b, void* y, int rows, int width, void* y_mx,
+                              int64_t ld_mx, void* stream);
+
+/*
  * (embed_ln, block_tail, layernorm) out_dtype AACLIP_FP8: the LayerNorm row (h / y)
  * is written as MX fp8 — e4m3 bytes [rows, width] plus an e8m0 scale per (row, 64
  * columns) in h_mx / y_mx [width/128][ld_mx >= rows][2], the A-operand format of

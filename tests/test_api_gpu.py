@@ -128,6 +128,30 @@ def test_harness_synthetic_mvtec_c4_vs_oracle(tmp_path):
     assert len(df) == 16 and df.iloc[-1]["class name"] == "Average"
 
 
+def test_harness_capture_with_live_pinned_loader(dev, model):
+    """get_predictions with a multi-worker, pin_memory DataLoader (the real-data harness
+    setting, test.py:243-245): the loader's pin-memory thread allocates pinned host memory
+    and queries events while AdaptedCLIP.predict captures its hipGraph on the second
+    same-shape batch (thread_local capture mode). Four batches of 2 (eager, capture,
+    replay, replay) plus a tail batch of 1; every map and score bit-identical to an eager
+    predict of the same images."""
+    import test as harness
+    from dataset import DOMAINS, get_dataset
+    ds = get_dataset("synthetic", 336, None, -1, "test", synthetic_n=9)["bottle"]
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, shuffle=False, num_workers=2, pin_memory=True)
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=torch.Generator(device=dev).manual_seed(3)),
+                                      dim=0).contiguous()
+    eng = model.visual_engine()
+    n_graphs = len(getattr(eng, "_graph_cache", {}))
+    with torch.no_grad():
+        masks, labels, preds, scores, names = harness.get_predictions(model, T, loader, dev, 336, dataset="synthetic")
+        assert len(getattr(eng, "_graph_cache", {})) == n_graphs + 1  # the batch-2 shape was captured
+        x = torch.stack([ds[i]["image"] for i in range(len(ds))]).to(dev)
+        m0, s0 = eng.predict(x, T, DOMAINS["synthetic"])
+    assert preds.shape == (9, 336, 336) and len(names) == 9 and labels.shape == (9,)
+    assert torch.equal(preds, m0) and torch.equal(scores, s0)
+
+
 def test_batched_text_anchors_equal_per_class(dev, model):
     """get_adapted_text_embedding encodes every prompt of the dataset in one call:
     each class's anchors must equal the per-class path bit for bit."""

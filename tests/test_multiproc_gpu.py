@@ -1,0 +1,44 @@
+"""The data-parallel path of config C3 (images sharded over ranks, one process per GPU,
+scores all-gathered) driven through the REAL HIP engine in two processes.
+
+A one-GPU box cannot host two RCCL ranks (RCCL refuses two ranks on one device), so the
+bench's rehearsal mode puts both ranks on cuda:0 over gloo: the same self-launch
+(torch.distributed.run as a child), shard_range slices of one seeded global batch, the
+per-step all-gather, max-over-ranks timing and the post-hoc self-check
+(parallel.verify_gather: every rank finds its own scores in the gathered vector, rank 0
+recomputes the other rank's shard with an eager one-stream predict and compares bit for
+bit) -- on VisualEngine outputs, not a CPU stand-in (tests/test_distributed_gloo.py).
+Reference: the per-batch loop being sharded, test.py:53-99.
+
+The bench is started as a FRESH child process (never an exec of this test process, which
+has initialised the GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_real_engine(dev):
+    env = dict(os.environ, AACLIP_BENCH_REHEARSAL="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-c5", "--no-modes", "--no-roofline", "--cpu-seconds", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    print({k: line[k] for k in ("value", "n_gpus", "ms_per_step")}, line["distributed"])
+    assert line["n_gpus"] == 2
+    assert line["config"]["global_batch"] == 64
+    d = line["distributed"]
+    assert d["world"] == 2 and d["backend"] == "gloo"
+    assert d["gather_verified"] and d["own_slice_verified"], d
+    assert d["checked_shard"]["rank"] == 1 and d["checked_shard"]["images"] == [32, 64]
+    assert line["step_outputs_verified"]["finite"] and line["step_outputs_verified"]["equal_to_one_stream_eager"]
