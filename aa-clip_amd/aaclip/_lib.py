@@ -48,6 +48,8 @@ SIGNATURES = {
     "aaclip_im2col": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "aaclip_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],
     "aaclip_block_tail": [_I, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _L, _P],
+    "aaclip_gemm_scores": [_I, _I, _I, _I, _P, _L, _P, _L, _I, _P, _I, _P, _L, _P],
+    "aaclip_anomaly_map_partials": [_P, _L, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P],
     "aaclip_layernorm": [_I, _P, _L, _P, _P, _P, _L, _I, _I, _P, _L, _P],
     "aaclip_residual_layernorm": [_I, _P, _P, _P, _P, _P, _I, _I, _P, _L, _P],
     "aaclip_text_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],

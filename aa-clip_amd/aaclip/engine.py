@@ -170,6 +170,10 @@ class VisualEngine:
         # the u workspace with no residual read, and ln_2 does x += d before normalising
         # (aaclip_residual_layernorm; the same fp32 add, bit-identical)
         self.defer_resid = os.environ.get("AACLIP_DEFER_RESID", "0") == "1"
+        # predict(): projections straight into map partials (aaclip_gemm_scores +
+        # aaclip_anomaly_map_partials) instead of segbuf rows + a stream over them;
+        # AACLIP_MAP_PARTIALS=0 restores the row path (A/B)
+        self.map_partials = os.environ.get("AACLIP_MAP_PARTIALS", "1") == "1"
 
     # ------------------------------------------------------------------ workspace
     def _workspace(self, B: int, S: int, slot: int = 0):
@@ -199,6 +203,11 @@ class VisualEngine:
             # patch cosine by ~1e-4 (x100 in the map) — the largest single bf16
             # term in the anomaly-map error budget, for ~15 us per batch of 32.
             segbuf=e(B * P, (L + 1) * EMBED, dt=torch.float32),
+            # predict() in the 16-bit modes: the level / det projections leave as anomaly-map
+            # partials (aaclip_gemm_scores: per row and 32 columns {||v||^2, v.t0, v.t1}),
+            # 384 B per (row, level) instead of 3 KB rows; segbuf is then only forward()'s
+            spart=e(B * P, (L + 1) * 4 * ops.SCORE_GROUPS, dt=torch.float32) if cdt != torch.float32 else None,
+            detrow=e(B * P, dt=torch.float32),
             # fp8 mode (MX): e4m3 GEMM inputs with e8m0 scales per (row, 64 columns):
             # a8/asc for the 1024-wide inputs (quantised from bf16), f8/fsc for the
             # 4096-wide GELU output (written in fp8 by the c_fc epilogue itself)
@@ -260,9 +269,11 @@ class VisualEngine:
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
     @_on_device
-    def forward_raw(self, x: torch.Tensor, slot: int = 0):
+    def forward_raw(self, x: torch.Tensor, slot: int = 0, T: torch.Tensor | None = None):
         """Run the visual tower; returns (seg_raw list of [B*P, 768] views,
-        det_raw [B*P, 768] view, workspace). Rows are unnormalised projections."""
+        det_raw [B*P, 768] view, workspace). Rows are unnormalised projections.
+        With T (predict, 16-bit modes) the projections are written as anomaly-map
+        partials against T into ws["spart"] instead, and (None, None, ws) is returned."""
         if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != x.shape[3] or x.shape[2] % PATCH:
             raise ValueError("input must be [B, 3, S, S] with S a multiple of 14")
         x = x.to(self.device, torch.float32).contiguous()
@@ -347,6 +358,13 @@ class VisualEngine:
                 ops.block_tail(X, n_tok, u=u, adapt_weight=self.i_w, ln=nxt, h=Hq if nxt else None,
                                post=self.ln_post, tap=tap, h_sc=Hsc)
         L = len(self.levels)
+        if T is not None and ws["spart"] is not None:
+            sp = ws["spart"]
+            G = 4 * ops.SCORE_GROUPS
+            for j in range(L):
+                ncol = self.w_seg[j].shape[0]
+                ops.gemm_scores(ws["taps"][j], self.w_seg[j], T, sp[:, j * G:j * G + ncol // 8], leaky=self.relu)
+            return None, None, ws
         sb = ws["segbuf"]
         for j in range(L):
             ncol = self.w_seg[j].shape[0]
@@ -393,6 +411,10 @@ class VisualEngine:
         6.4; the one-pass entry stays in the ABI, bit-identical (tests). The map itself is
         two launches (patch scores, then blur + upsample); AACLIP_MAP_FUSED=1 selects the
         one-launch aaclip_anomaly_map_fused (same bits, measured 2x slower in the step)."""
+        if seg_raw is None:  # projections as partials (forward_raw with T)
+            ops.anomaly_map_partials(ws["spart"], len(self.levels), out_map, ws["grid"], g=ws["g"], ksize=k, sigma=s,
+                                     det_ws=ws["detrow"], score=out_score)
+            return
         if self.map_fused:
             ops.anomaly_map_fused(seg_raw, T, out_map, ws["grid"], ws["bandcnt"], g=ws["g"], ksize=k, sigma=s)
         else:
@@ -440,7 +462,7 @@ class VisualEngine:
         for v in sizes:
             bounds.append(bounds[-1] + v)
         if len(sizes) == 1:
-            seg_raw, det_raw, ws = self.forward_raw(x, slot=_slot0)
+            seg_raw, det_raw, ws = self.forward_raw(x, slot=_slot0, T=T if self.map_partials else None)
             self._tail(seg_raw, det_raw, ws, T, ws["map"], ws["score"], k, s)
             return ws["map"], ws["score"]
         key = ("out", B, S, _slot0)
@@ -476,7 +498,8 @@ class VisualEngine:
                 b0, b1 = bounds[i], bounds[i + 1]
                 st = sts[i % nstreams]
                 with torch.cuda.stream(st):
-                    seg_raw, det_raw, ws = self.forward_raw(x[b0:b1], slot=_slot0 + i % nstreams)
+                    seg_raw, det_raw, ws = self.forward_raw(x[b0:b1], slot=_slot0 + i % nstreams,
+                                                            T=T if self.map_partials else None)
                     self._tail(seg_raw, det_raw, ws, T, out_map[b0:b1], out_score[b0:b1], k, s)
         for st, ev in zip(sts, done):
             ev.record(st)

@@ -543,6 +543,52 @@ def anomaly_map(levels, T, out, grid_ws, *, g, ksize, sigma, normalize=True):
     return out
 
 
+SCORE_GROUPS = 768 // 32  # float4 partials per (row, level) written by gemm_scores
+
+
+def gemm_scores(a: torch.Tensor, w: torch.Tensor, T: torch.Tensor, part: torch.Tensor, *, leaky=False):
+    """Level projection straight into anomaly-map partials (aaclip_gemm_scores): for
+    v = LeakyReLU?(a @ w.T), part[m, 4g:4g+4] = {||v||^2, v.t0, v.t1, 0} over columns
+    32g..32g+31, t = T[c % 768]. part: fp32 view [M, >= N/8] (unit column stride)."""
+    _dev(a, w, T, part)
+    _rowmajor(a, "a")
+    _rowmajor(w, "w")
+    _rowmajor(part, "part")
+    if a.dtype not in (torch.bfloat16, torch.float16) or w.dtype != a.dtype:
+        raise TypeError("gemm_scores: 16-bit operands of one dtype")
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K or part.shape[0] != M or part.shape[1] < N // 8 or part.dtype != torch.float32:
+        raise ValueError("gemm_scores shape mismatch")
+    if T.dtype != torch.float32 or not T.is_contiguous() or T.shape != (768, 2):
+        raise ValueError("gemm_scores: T must be contiguous fp32 [768, 2]")
+    _launch(f"gemm N{N} K{K} scores" + (" leaky" if leaky else ""), lambda: gemm_plan(dtag(a), M, N, K),
+            2.0 * M * N * K, (M * K + N * K) * a.element_size() + M * N // 8 * 4, "aaclip_gemm_scores", dtag(a), M,
+            N, K, _ptr(a), a.stride(0), _ptr(w), w.stride(0), 4 if leaky else 0, _ptr(T), 768, _ptr(part),
+            part.stride(0), _stream())
+
+
+def anomaly_map_partials(part, n_levels, out, grid_ws, *, g, ksize, sigma, det_ws=None, score=None):
+    """Map (+ image score when det_ws / score are given) from gemm_scores partials
+    (aaclip_anomaly_map_partials): part [B*g*g, >= (n_levels + det) * 96] fp32."""
+    _dev(part, out, grid_ws, det_ws, score)
+    _rowmajor(part, "part")
+    B, S, S2 = out.shape
+    rows = B * g * g
+    det = det_ws is not None
+    if part.shape[0] != rows or part.shape[1] < (n_levels + det) * 4 * SCORE_GROUPS or S != S2:
+        raise ValueError("anomaly_map_partials shape mismatch")
+    if grid_ws.numel() < rows or (det and (det_ws.numel() < rows or score is None or score.numel() < B)):
+        raise ValueError("anomaly_map_partials workspace too small")
+    if not out.is_contiguous():
+        raise ValueError("anomaly_map_partials output must be contiguous")
+    nb = rows * (n_levels + det) * 4 * SCORE_GROUPS * 4 + B * S * S * 4 + 2 * rows * 4
+    _launch("anomaly_map", "anomaly_map (partial_scores + blur_upsample)", 0.0, nb, "aaclip_anomaly_map_partials",
+            _ptr(part), part.stride(0), n_levels, int(det), B, g, S, ksize, float(sigma), _ptr(grid_ws),
+            _ptr(det_ws), _ptr(out), _ptr(score), _stream())
+    return out
+
+
 def map_band_counters(B: int, S: int, device) -> torch.Tensor:
     """Zeroed band counters for anomaly_map_fused (B * ceil(S / 8) int32); every fused call
     leaves them zero again. One set per concurrently running call (per chunk workspace)."""

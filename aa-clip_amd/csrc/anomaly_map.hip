@@ -338,6 +338,71 @@ __global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, fl
                   threadIdx.x);
 }
 
+// Stage 1 from GEMM partials (aaclip_gemm_scores wrote, per patch row and 32-column group
+// g of each level, {||v||^2, v.t0, v.t1}): one HALF-wave per patch row, lane q < 24 holds
+// group q of every level (one float4 per level), fixed-order butterfly sums over the 32
+// lanes (every lane ends with the same bits), then patch_row_score's normalise + anchor
+// arithmetic (normalize = 1). The det level (with_det) leaves d.t1 / ||d|| per row for
+// the image score. 1.9 KB read per C2 patch row instead of 15 KB of projected rows.
+constexpr int kGroups = 768 / 32;  // 32-column groups per level
+
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+  return v;
+}
+
+template <int NLMAX>
+__global__ __launch_bounds__(256) void partial_scores_kernel(const float* __restrict__ part, int64_t ld, int nl,
+                                                             int with_det, int rows, float* __restrict__ grid,
+                                                             float* __restrict__ det_rows) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (row >= rows) return;
+  const float* pr = part + (size_t)row * ld + 4 * lane;
+  const int nt = nl + with_det;
+  float4_t v[NLMAX + 1];
+#pragma unroll
+  for (int l = 0; l <= NLMAX; ++l)
+    if (l < nt) v[l] = lane < kGroups ? *(const float4_t*)(pr + l * 4 * kGroups) : float4_t{0.f, 0.f, 0.f, 0.f};
+  float acc = 0.f;
+#pragma unroll
+  for (int l = 0; l <= NLMAX; ++l) {
+    if (l < nt) {
+      const float ss = half_sum(v[l][0]), a0 = half_sum(v[l][1]), a1 = half_sum(v[l][2]);
+      const float inv = 1.0f / fmaxf(sqrtf(ss), 1e-12f);
+      if (l < nl) {
+        const float A0 = 100.0f * (a0 * inv), A1 = 100.0f * (a1 * inv);
+        acc += (A1 + 1.0f - A0) / 2.0f;
+      } else if (lane == 0) {
+        det_rows[row] = a1 * inv;  // normalize(d) . t1
+      }
+    }
+  }
+  if (lane == 0) grid[row] = acc;
+}
+
+// Stage 2 + the image score: blur_upsample_kernel's bands, and the band-0 wave of each
+// image also reduces its n_patch det rows (fixed order: lane-strided sums, then the wave
+// butterfly) to score[b] = (mean_p normalize(d_p).t1 + 1) / 2 (test.py:83-84).
+template <int K>
+__global__ __launch_bounds__(64) void blur_upsample_score_kernel(const float* grid, float* out, int g, int S,
+                                                                 int ksize_rt, Gauss gw, float scale, int xrows,
+                                                                 int brows, const float* det_rows, int n_patch,
+                                                                 float* score) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  if (blockIdx.x == 0 && det_rows) {
+    const float* d = det_rows + (size_t)blockIdx.y * n_patch;
+    float t = 0.f;
+    for (int p = threadIdx.x; p < n_patch; p += 64) t += d[p];
+    t = wave_sum(t);
+    if (threadIdx.x == 0) score[blockIdx.y] = (t / (float)n_patch + 1.0f) / 2.0f;
+  }
+  blur_band<1, K>(grid, out, blockIdx.y, blockIdx.x, g, S, ksize_rt, gw, 0, scale, xrows, brows, smem, threadIdx.x);
+}
+
 // Source grid rows [x_lo, x_hi] one output band reads (blur_band: the bilinear taps'
 // rows r_lo..r_hi and their blur neighbourhood, clamped; reflected indices stay inside).
 __device__ __forceinline__ void band_rows(int band, int g, int S, int ksize, float scale, int& x_lo, int& x_hi) {
@@ -653,6 +718,43 @@ extern "C" int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n
                                normalize, 0, 0, grid_ws, stream);
   if (rc) return rc;
   return aaclip_blur_upsample(grid_ws, out, batch, 1, g, out_size, ksize, sigma, 0, stream);
+}
+
+extern "C" int aaclip_anomaly_map_partials(const float* part, int64_t ld_part, int n_levels, int with_det,
+                                           int batch, int g, int out_size, int ksize, float sigma, float* grid_ws,
+                                           float* det_ws, float* out, float* score, void* stream) {
+  AACLIP_REQUIRE(part && grid_ws && out && batch > 0 && n_levels >= 1 && n_levels <= kMaxLevels);
+  AACLIP_REQUIRE(with_det == 0 || (with_det == 1 && det_ws && score));
+  AACLIP_REQUIRE(ld_part >= (int64_t)(n_levels + with_det) * 4 * kGroups && ld_part % 4 == 0);
+  AACLIP_REQUIRE(((uintptr_t)part % 16) == 0);
+  AACLIP_REQUIRE(blur_upsample_args_ok(1, g, out_size, ksize));  // before the first launch
+  const int rows = batch * g * g;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_levels <= 4)
+    partial_scores_kernel<4><<<ceil_div(rows, 8), 256, 0, s>>>(part, ld_part, n_levels, with_det, rows, grid_ws,
+                                                                det_ws);
+  else
+    partial_scores_kernel<kMaxLevels><<<ceil_div(rows, 8), 256, 0, s>>>(part, ld_part, n_levels, with_det, rows,
+                                                                         grid_ws, det_ws);
+  AACLIP_CHECK_LAUNCH();
+  const Gauss gw = ksize > 0 ? gaussian_weights(ksize, sigma) : Gauss{};
+  const float scale = (float)(g - 1) / (float)(out_size - 1);
+  const int span = (int)(scale * (float)(kBand - 1)) + 4;  // as launch_blur_upsample
+  const int brows = min(g, span);
+  const int xrows = min(g, brows + 2 * (ksize / 2));
+  const size_t lds = blur_upsample_lds(1, g, out_size, ksize);
+  const dim3 grd(ceil_div(out_size, kBand), batch);
+  const float* dr = with_det ? det_ws : nullptr;
+#define BS_LAUNCH(K)                                                                                      \
+  blur_upsample_score_kernel<K><<<grd, 64, lds, s>>>(grid_ws, out, g, out_size, ksize, gw, scale, xrows, brows, \
+                                                     dr, g * g, score)
+  if (ksize == 0) BS_LAUNCH(0);
+  else if (ksize == 7) BS_LAUNCH(7);
+  else if (ksize == 9) BS_LAUNCH(9);
+  else BS_LAUNCH(-1);
+#undef BS_LAUNCH
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
 }
 
 extern "C" int aaclip_anomaly_map_fused(int in_dtype, const void* const* levels, int n_levels, int64_t ld,

@@ -49,7 +49,12 @@ struct GemmArgs {
   int64_t ld_amx;
   uint8_t* c_mx;         // fp8 MX output: e8m0 scale per (row, 64-column block), [N/128][ld_cmx][2]
   int64_t ld_cmx;
+  const float* anchors;  // score-partials output (OUTM 3): text anchors T [t_period][2] (normal, abnormal)
+  int t_period;          // column c uses anchor row c % t_period (the level width, 768)
 };
+
+// out_dtype tag of the score-partials output (aaclip_gemm_scores; never a public dtype)
+constexpr int kOutScores = 100;
 
 // smallest e with amax * 2^-e <= 448 (largest finite e4m3): the e8m0 block scale
 __device__ __forceinline__ int mx_exp(float amax) {
@@ -68,6 +73,16 @@ __device__ __forceinline__ float max_over_fq(float v) {
   v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
   auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// sum over the 4 lanes {c, c+16, c+32, c+48} in a fixed association, (fq0 + fq1) + (fq2 + fq3)
+// with the pairs' operands swapped on the partner lanes -- fp32 addition commutes, so all
+// four lanes end with the same bits
+__device__ __forceinline__ float sum_over_fq(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
 // 4x4 dword transpose across the lane groups fq = lane/16: on entry lane fq holds
@@ -207,6 +222,7 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
                                               int lane) {
   static_assert(RN % 2 == 0, "column tiles are paired");
   static_assert(OUTM != 2 || RN == 4, "fp8 MX output: one 64-column block per wave");
+  static_assert(OUTM != 3 || RN == 2 || RN == 4, "score partials: one or two 32-column groups per wave");
   constexpr bool BF16OUT = OUTM == 1;
   const int fr = lane & 15, fq = lane >> 4;
   const int epi = EPI >= 0 ? EPI : a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
@@ -217,6 +233,17 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
 #pragma unroll
   for (int j = 0; j < RN; ++j)
     bias[j] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)(a.bias + ncol + 16 * j) : float4_t{0.f, 0.f, 0.f, 0.f};
+  // OUTM 3 (score partials): this lane's anchor values, t0 / t1 of columns ncol + 16 j + e
+  float4_t ta0[RN], ta1[RN];
+  if constexpr (OUTM == 3) {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int c = (ncol + 16 * j) % a.t_period;
+      const float4_t lo = *(const float4_t*)(a.anchors + 2 * c), hi = *(const float4_t*)(a.anchors + 2 * c + 4);
+      ta0[j] = float4_t{lo[0], lo[2], hi[0], hi[2]};
+      ta1[j] = float4_t{lo[1], lo[3], hi[1], hi[3]};
+    }
+  }
   float4_t wsc[RN];  // fp8: per-column weight scales of this lane's 4 columns in tile j
   if constexpr (SCALED) {
 #pragma unroll
@@ -271,6 +298,31 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
     }
     const int m = mw + 16 * i + fr;
     const size_t orow = (size_t)out_row(min(m, a.M - 1));
+    if constexpr (OUTM == 3) {
+      // anomaly-map partials of row m over each 32-column group (column tiles 2q, 2q+1):
+      // ||v||^2, v.t0, v.t1 -- lane-local fixed-order FMA chains over its 8 values, then
+      // the fixed-order sum over the 4 lane groups. Every tile family holds the same
+      // lane layout and 32-column-aligned groups, so the partials (and the map) do not
+      // depend on which family ran. Lane group q < RN/2 stores group q as one float4.
+      float4_t pr[RN / 2];
+#pragma unroll
+      for (int q = 0; q < RN / 2; ++q) {
+        float ss = 0.f, x0 = 0.f, x1 = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float u = v[2 * q + jj][e];
+            ss = fmaf(u, u, ss);
+            x0 = fmaf(u, ta0[2 * q + jj][e], x0);
+            x1 = fmaf(u, ta1[2 * q + jj][e], x1);
+          }
+        pr[q] = float4_t{sum_over_fq(ss), sum_over_fq(x0), sum_over_fq(x1), 0.f};
+      }
+      if (m < a.M && fq < RN / 2)
+        *(float4_t*)((float*)a.C + orow * a.ldc + (nw >> 3) + 4 * fq) = (fq == 0) ? pr[0] : pr[RN / 2 - 1];
+      continue;
+    }
     if constexpr (OUTM == 2) {
       float amax = 0.f;
 #pragma unroll
@@ -485,7 +537,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   const int mw = m0 + wm * TM, nw = n0 + wn * TN;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
   constexpr int SC = Q == 1 ? 1 : (Q == 2 ? 2 : 0);
-  const int outm = a.out_dtype == AACLIP_F32 ? 0 : (a.out_dtype == AACLIP_FP8 ? 2 : 1);
+  const int outm =
+      a.out_dtype == AACLIP_F32 ? 0 : (a.out_dtype == AACLIP_FP8 ? 2 : (a.out_dtype == kOutScores ? 3 : 1));
 #define EPI_CASE(OM, E)                                                \
   if (outm == (OM) && key == (E)) {                                    \
     wave_epilogue<RM, RN, OM, E, SC, H16>(a, acc, mw, nw, lane);       \
@@ -501,6 +554,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   EPI_CASE(0, AACLIP_EPI_LEAKY)                                       // adapters, seg/det proj
   EPI_CASE(0, 0)                                                      // seg/det proj (no relu)
   EPI_CASE(0, EPI_REMAP)                                              // patch embedding
+  if constexpr (!FP8 && (BN / WN == 64 || BN / WN == 32)) {
+    EPI_CASE(3, AACLIP_EPI_LEAKY)                                     // seg/det proj -> map partials
+    EPI_CASE(3, 0)
+  }
   if constexpr (BN / WN == 64) {
     EPI_CASE(2, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)                    // c_fc -> fp8 MX c_proj input
     EPI_CASE(2, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)
@@ -763,6 +820,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else if (a.out_dtype == kOutScores) {  // seg/det proj -> map partials (no stores to overlap)
+      if (key == AACLIP_EPI_LEAKY)
+        wave_epilogue<RM, RN, 3, AACLIP_EPI_LEAKY, 0, H16>(a, acc, mw, nw, lane);
+      else
+        wave_epilogue<RM, RN, 3, 0, 0, H16>(a, acc, mw, nw, lane);
     } else {
 #define EPI_CASE(BF, E, NS)                                               \
   if (bf16_out == (BF) && key == (E)) {                                   \
@@ -1368,6 +1430,42 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
   gemm_f32_kernel<<<a.tiles_m * a.tiles_n, 256, 0, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
+}
+
+extern "C" int aaclip_gemm_scores(int in_dtype, int M, int N, int K, const void* A, int64_t lda, const void* W,
+                                  int64_t ldw, int epilogue, const float* T, int t_period, float* part,
+                                  int64_t ld_part, void* stream) {
+  AACLIP_REQUIRE(in_dtype == AACLIP_BF16 || in_dtype == AACLIP_F16);
+  AACLIP_REQUIRE(A && W && T && part && M >= 0 && N > 0 && K > 0 && K % 64 == 0 && N % 256 == 0);
+  AACLIP_REQUIRE(t_period > 0 && t_period % 64 == 0 && ld_part >= N / 8 && ld_part % 4 == 0);
+  AACLIP_REQUIRE(lda >= K && ldw >= K && lda % 8 == 0 && ldw % 8 == 0);
+  AACLIP_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0 && ((uintptr_t)part % 16) == 0 &&
+                 ((uintptr_t)T % 16) == 0);
+  AACLIP_REQUIRE(epilogue == 0 || epilogue == AACLIP_EPI_LEAKY);
+  if (M == 0) return AACLIP_OK;
+  GemmArgs a{A, W, part, nullptr, nullptr, nullptr, lda, ldw, ld_part, 0, 0, M, N, K, epilogue,
+             kOutScores, 0, 0, 0, 0, 0, g_group_m, g_setprio, g_dbg & 1,
+             nullptr, nullptr, nullptr, 0, nullptr, 0, T, t_period};
+  hipStream_t s = (hipStream_t)stream;
+  const bool h16 = in_dtype == AACLIP_F16;
+  const bool fits = (int64_t)M * lda * 2 < (1ll << 31) && (int64_t)N * ldw * 2 < (1ll << 31);
+  // the same per-shape choice as aaclip_gemm (same K order, same bits); the A/B-only
+  // families without this epilogue (persistent 8-phase, two-workgroup) take the 8-phase one
+  switch (choose16(in_dtype, M, N, K, fits)) {
+    case KERN_256x256:
+      return h16 ? launch_bf16<256, 256, 2, 4, 0, true>(a, s) : launch_bf16<256, 256, 2, 4, 0, false>(a, s);
+    case KERN_320x256:
+      return h16 ? launch_bf16<320, 256, 2, 4, 0, true>(a, s) : launch_bf16<320, 256, 2, 4, 0, false>(a, s);
+    case KERN_128x128:
+      return h16 ? launch_bf16<128, 128, 2, 2, 0, true>(a, s) : launch_bf16<128, 128, 2, 2, 0, false>(a, s);
+    case KERN_64x64:
+      return h16 ? launch_bf16<64, 64, 2, 2, 0, true>(a, s) : launch_bf16<64, 64, 2, 2, 0, false>(a, s);
+    case KERN_256x128:
+      return h16 ? launch_bf16<256, 128, 4, 2, 0, true>(a, s) : launch_bf16<256, 128, 4, 2, 0, false>(a, s);
+    default:
+      if (!fits) return h16 ? launch_bf16<320, 256, 2, 4, 0, true>(a, s) : launch_bf16<320, 256, 2, 4, 0, false>(a, s);
+      return h16 ? launch_bf16_8ph<true>(a, s) : launch_bf16_8ph<false>(a, s);
+  }
 }
 
 extern "C" int aaclip_gemm_fp8(int out_dtype, int M, int N, int K, const void* A, int64_t lda,

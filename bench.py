@@ -411,6 +411,11 @@ def map_from_profile(p1, p2):
            "traffic": traffic, "traffic_source": src, "avg_launch_us": m["avg_launch_us"],
            "bytes_per_launch": m["bytes"] / m["launches"],
            "context": "in-step, one stream: the B=32 map after the level projections, HIP events around the op"}
+    sc = p1["by_op"].get("image_score")
+    out["map_plus_score_us"] = round((m["ms"] + (sc["ms"] if sc else 0.0)) / m["launches"] * 1e3, 2)
+    out["form"] = ("partials: the level/det projection GEMMs emit per-(row, 32-column) {||v||^2, v.t0, v.t1} "
+                   "(aaclip_gemm_scores), the map + image score read those (aaclip_anomaly_map_partials)"
+                   if "partial" in kern else "rows: the map and the image score stream the projected rows")
     if p2 is not None:
         m2 = p2["by_op"]["anomaly_map"]
         out["in_step_2stream"] = {"avg_launch_us": m2["avg_launch_us"], "GBs": m2["GBs"],

@@ -77,6 +77,24 @@ int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K,
                 int row_group, int row_group_out, int row_offset, void* stream);
 
 /*
+ * Level projection straight into anomaly-map partials (the predict path: the full
+ * projected rows are never written):
+ *   v = epilogue(A[M,K] . W[N,K]^T)   (epilogue 0 or AACLIP_EPI_LEAKY)
+ *   part[m][g] = { sum ||v||^2, sum v.t0, sum v.t1, 0 } over columns 32g .. 32g+31
+ * with t0/t1 = T[c % t_period][0/1] (T [t_period][2] fp32: normal, abnormal anchor),
+ * as fp32 float4 per (row, 32-column group): part [M][ld_part >= N/8] floats.
+ * Each group is summed in a fixed order that does not depend on the tile family, so
+ * the partials of a row are the same whatever the batch. 16-bit in_dtype only;
+ * K % 64 == 0, N % 256 == 0, t_period % 64 == 0.
+ * Replaces: seg_proj / det_proj (adapter.py:107-110) + the row norms and anchor dots
+ * of calculate_similarity_map (forward_utils.py:197-202) and of the image score
+ * (test.py:83-84).
+ */
+int aaclip_gemm_scores(int in_dtype, int M, int N, int K, const void* A, int64_t lda,
+                       const void* W, int64_t ldw, int epilogue, const float* T, int t_period,
+                       float* part, int64_t ld_part, void* stream);
+
+/*
  * fp8 GEMM (config C5: fp8 MFMA weights):
  *   C[M,N] = epilogue( a_scale[m] * w_scale[n] * (A8[M,K] . W8[N,K]^T) )
  * A8, W8: OCP e4m3 bytes (gfx950 FP8), per-row / per-output-channel fp32 scales
@@ -343,6 +361,23 @@ int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n_levels, in
 int aaclip_anomaly_map_fused(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
                              const float* T, int batch, int g, int channels, int out_size, int ksize,
                              float sigma, float* grid_ws, int* band_counters, float* out, void* stream);
+
+/*
+ * The predict path's map + image score from aaclip_gemm_scores partials (the level
+ * projections are never written as rows): part [batch*g*g][ld_part] fp32 holds, per
+ * patch row, n_levels levels (+ the det projection when with_det) of 24 float4
+ * partials {||v||^2, v.t0, v.t1, 0} (one per 32 columns of the 768). Stage 1 sums each
+ * level's 24 partials in a fixed order, normalises and forms the level-summed test
+ * score grid (as aaclip_patch_scores, normalize = 1) into grid_ws (>= batch*g*g) and,
+ * with_det, normalize(d).t1 per row into det_ws (>= batch*g*g); stage 2 is
+ * aaclip_blur_upsample (out [batch, S, S]) plus score[b] = (mean_p det_ws + 1) / 2.
+ * Every argument is checked before the first launch.
+ * Replaces: test.py:83-93 + forward_utils.py:196-213 after the projections.
+ */
+int aaclip_anomaly_map_partials(const float* part, int64_t ld_part, int n_levels, int with_det,
+                                int batch, int g, int out_size, int ksize, float sigma,
+                                float* grid_ws, float* det_ws, float* out, float* score,
+                                void* stream);
 
 /*
  * Image-level score: det[b] = mean_p normalize(det_raw[b*n_patch+p]) and
