@@ -383,6 +383,57 @@ def test_attention_spec_equals_split(dev, dt, B, N, H, spikes):
     assert err < (3e-2 if dt == torch.bfloat16 else 4e-3), err
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (1, 1025, 16, False), (2, 72, 4, False),
+                                          (1, 64, 2, False), (3, 136, 2, False), (2, 129, 4, False),
+                                          (5, 577, 2, False),
+                                          # not the 32x32 kernel's shapes: fall back to the 16x16 one
+                                          (3, 77, 12, True), (2, 73, 4, False), (2, 5, 2, False)])
+def test_attention_32x32_pipelined(dev, dt, B, N, H, causal):
+    """Variant 5 (attn32_kernel: v_mfma_f32_32x32x16, S(t+1) = K(t+1).Q^T beside P(t)'s
+    exponentials, 3-slot ring) against float64, every tile count parity (odd / even, the
+    loop is unrolled by two), the inline 1..8-key tail, a single tile, query tails."""
+    torch.manual_seed(B * N + H + 5)
+    qkv = (torch.randn(B * N, 3 * H * 64, device=dev) * 1.5).to(dt)
+    out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
+    _lib.call("aaclip_set_attn_variant", 5)
+    try:
+        ops.attention(qkv, out, B, N, H, causal=causal)
+    finally:
+        _lib.call("aaclip_set_attn_variant", 0)
+    err = (out.double() - _attn_ref(qkv, B, N, H, causal)).abs().max().item()
+    assert err < (3e-2 if dt == torch.bfloat16 else 4e-3), err
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_attention_32x32_rescale_paths(dev, dt):
+    """Variant 5 under the deferred-max branch: a slowly rising key norm (deferred, p up to
+    256), late spikes at several tiles (the rescale of the pipelined S(t+1), O and l), and
+    a NaN-free result equal to float64 within the 16-bit bound; also with q prescaled."""
+    B, N, H = 2, 577, 4
+    g = torch.Generator(device=dev).manual_seed(12)
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev, generator=g) * 0.1
+    qkv[:, :64] = 1.0
+    ramp = torch.linspace(0.0, 0.6, N, device=dev).repeat(B)
+    qkv[:, H * 64:H * 64 + 64] += ramp[:, None]
+    for i, row in enumerate((100, 300, 500, 576)):
+        qkv[row, H * 64 + 64:H * 64 + 128] = 2.0 + i  # head 1 keys: spikes in tiles 1, 4, 7 and the tail
+        qkv[:, 64:128] = 1.0
+    x = qkv.to(dt)
+    for pre in (False, True):
+        xin, ref_in = (_prescale_q(x, H) if pre else (x, x.double()))
+        if pre and dt == torch.float16:
+            xin = xin.to(dt)
+        out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
+        _lib.call("aaclip_set_attn_variant", 5)
+        try:
+            ops.attention(xin, out, B, N, H, q_prescaled=pre)
+        finally:
+            _lib.call("aaclip_set_attn_variant", 0)
+        err = (out.double() - _attn_ref(ref_in, B, N, H, False)).abs().max().item()
+        assert torch.isfinite(out).all() and err < (3e-2 if dt == torch.bfloat16 else 4e-3), (pre, err)
+
+
 SL2 = 0.125 * 1.4426950408889634  # log2(e)/sqrt(64), what the engine folds into the Q projection
 
 
