@@ -1181,17 +1181,23 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
         }
     }
   }
-  if (q0 + r >= N) return;
+  // O[q][d]: the lane holds d = 32 db + 8 k4 + 4 hh + i; the two half-waves' 8-byte pieces
+  // of column groups k4, k4 + 1 are exchanged with v_permlane32_swap so every lane stores 16
+  // contiguous bytes (half 0: columns 8 k4 .. +7, half 1: 8 (k4 + 1) .. +7)
   const float inv = 1.0f / l_acc[0];
-  uint16_t* op = out + ((size_t)b * N + q0 + r) * HDt + h * HD_;
+  const bool qok = q0 + r < N;
+  uint16_t* op = out + ((size_t)b * N + min(q0 + r, N - 1)) * HDt + h * HD_;
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
-      uint2 w;
-      w.x = pack_h16x2<H16>(o[db][4 * k4] * inv, o[db][4 * k4 + 1] * inv);
-      w.y = pack_h16x2<H16>(o[db][4 * k4 + 2] * inv, o[db][4 * k4 + 3] * inv);
-      *(uint2*)(op + 32 * db + 8 * k4 + 4 * hh) = w;
+    for (int k4 = 0; k4 < 4; k4 += 2) {
+      uint32_t a0 = pack_h16x2<H16>(o[db][4 * k4] * inv, o[db][4 * k4 + 1] * inv);
+      uint32_t a1 = pack_h16x2<H16>(o[db][4 * k4 + 2] * inv, o[db][4 * k4 + 3] * inv);
+      uint32_t b0 = pack_h16x2<H16>(o[db][4 * k4 + 4] * inv, o[db][4 * k4 + 5] * inv);
+      uint32_t b1 = pack_h16x2<H16>(o[db][4 * k4 + 6] * inv, o[db][4 * k4 + 7] * inv);
+      const auto x = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto y = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      if (qok) *(uint4*)(op + 32 * db + 8 * k4 + 8 * hh) = uint4{x[0], y[0], x[1], y[1]};
     }
 }
 
