@@ -1014,7 +1014,10 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
   if (active) {
     short8_t kf[2][4];
     read_k(0, kf);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) lgkm_wait<0>(kf[kb][ks]);  // tied: no MFMA reads them earlier
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
