@@ -882,12 +882,16 @@ __device__ __forceinline__ void lgkm_wait(short4_t (&d)[4]) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]) : "i"(N));
 }
 
-template <bool H16>
-__global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+// OCC: workgroups per CU the registers are sized for (2: 4-slot ring, tiles t+1..t+3 in
+// flight; 3: 3-slot ring, ~25 VGPRs spilled -- measured); MSUM: row sums
+// by a ones-operand MFMA (4 per tile, bf16-rounded p like the numerator) instead of f32
+// VALU adds of the exponentials.
+template <bool H16, int OCC, bool MSUM>
+__global__ __launch_bounds__(256, OCC) void attn32_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                         int batch, int N, int H, int flags) {
   using V8 = h16x8_t<H16>;
   using E = h16_t<H16>;
-  constexpr int NS = 4, SLOT = 2 * KT * 128;  // [slot][K|V][64 rows][128 B]; tiles t+1..t+3 in flight
+  constexpr int NS = OCC == 2 ? 4 : 3, SLOT = 2 * KT * 128;  // [slot][K|V][64 rows][128 B]
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -961,15 +965,21 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
   const int tail_keys = N % KT;
   const bool tail_inline = (flags & AACLIP_ATTN_CAUSAL) == 0 && tail_keys <= 8;
   const int nt = N / KT;  // full tiles (the caller guarantees tail_inline)
-  f32x16_t o[2], l_acc, splat, sa[2], sb[2];  // sa / sb: the two score sets
+  f32x16_t o[2], splat, sa[2], sb[2];  // sa / sb: the two score sets
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     o[0][i] = 0.f;
     o[1][i] = 0.f;
-    l_acc[i] = 0.f;
   }
+  // row sums: this lane's half of the query's keys, f32 adds of the exponentials (two
+  // chains); the halves are combined at the end. (A ones-operand 32x32 MFMA would cost 4
+  // MFMAs = 128 matrix cycles per tile for one useful row of 32.)
+  float l0 = 0.f, l1 = 0.f;
   float m_run = 0.f;
+  f32x16_t l_acc;  // MSUM: every row of it holds the sums
   V8 ones;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) l_acc[i] = 0.f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (E)1.f;
 
@@ -1000,16 +1010,21 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) kf[1][ks] = lds_b128<4096>(ka[ks] + so);
   };
+  auto read_k_half = [&](uint32_t so, short8_t (&kf)[4], auto kb) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) kf[ks] = lds_b128<4096 * decltype(kb)::value>(ka[ks] + so);
+  };
 
   // prologue: tiles 0..2 in flight, S(0) with a zero accumulator, the running max from
   // tile 0 (every query has 64 valid keys there), S(0) -= m
   stage(0, 0);
   if (nt > 1) stage(1, 1);
-  if (nt > 2) stage(2, 2);
-  if (nt > 2)
+  if (NS == 4 && nt > 2) {
+    stage(2, 2);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else
+  } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   if (active) {
     short8_t kf[2][4];
@@ -1037,9 +1052,10 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
   // one tile: P(t) from sc, S(t+1) into sn (the score sets swap roles every tile; the loop
   // is unrolled by two so they stay in fixed registers, no copies)
   auto step = [&](int t, int cur, f32x16_t (&sc)[2], f32x16_t (&sn)[2]) {
-    const int nxt = (cur + 1) & (NS - 1);
-    const bool deep = t + 3 < nt;
-    if (deep) stage(t + 3, (cur + 3) & (NS - 1));
+    const int nxt = cur == NS - 1 ? 0 : cur + 1;
+    const int ahead = NS - 1;  // tiles issued ahead of t
+    const bool deep = t + ahead < nt;
+    if (deep) stage(t + ahead, cur == 0 ? NS - 1 : cur - 1);
     if (active) {
       const bool more = t + 1 < nt;
       // phase A: S(t+1) = K(t+1) . Q^T (8 MFMAs, slot nxt: a stale slot after the last
@@ -1048,11 +1064,17 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
       // beside the last 1.5 packs and S(t+1)'s max tree. sched_barrier fences pin each
       // group's VALU next to its MFMA (hipcc otherwise bunches the waits and the VALU).
       short8_t kf[2][4];
-      read_k(nxt * SLOT, kf);
+      read_k_half(nxt * SLOT, kf[0], std::integral_constant<int, 0>{});
       V8 pf[2][2];
       auto half = [&](V8& v, const f32x16_t& sv, int st, int hf) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[4 * hf + j] = (E)__builtin_amdgcn_exp2f(sv[8 * st + 4 * hf + j]);
+        for (int j = 0; j < 4; ++j) {
+          const float e = __builtin_amdgcn_exp2f(sv[8 * st + 4 * hf + j]);
+          v[4 * hf + j] = (E)e;
+          if constexpr (!MSUM) {
+            if (j & 1) l1 += e; else l0 += e;
+          }
+        }
       };
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
 #define QK_MFMA(KB, KS, N)                                                                                 \
@@ -1061,9 +1083,10 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
       half(pf[0][0], sc[0], 0, 0);  // covers the K reads' LDS latency
       half(pf[0][0], sc[0], 0, 1);
       FENCE();
-      QK_MFMA(0, 0, 7)
+      QK_MFMA(0, 0, 3)
       FENCE();
-      QK_MFMA(0, 1, 6)
+      QK_MFMA(0, 1, 2)
+      read_k_half(nxt * SLOT, kf[1], std::integral_constant<int, 1>{});
       half(pf[0][1], sc[0], 1, 0);
       FENCE();
       QK_MFMA(0, 2, 5)
@@ -1097,7 +1120,7 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
           o[db] = mfma32(__builtin_bit_cast(V8, short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}), p,
                          o[db]);
         }
-        l_acc = mfma32(ones, p, l_acc);
+        if constexpr (MSUM) l_acc = mfma32(ones, p, l_acc);
       };
       read_v(std::integral_constant<int, 0>{}, vr[0]);  // (kb, st) = (0, 0): rows 0..
       read_v(std::integral_constant<int, 2>{}, vr[1]);  // (0, 1): rows 16..
@@ -1129,15 +1152,20 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
         for (int i = 0; i < 16; ++i) {
           o[0][i] *= alpha;
           o[1][i] *= alpha;
-          l_acc[i] *= alpha;
           sn[0][i] -= d;
           sn[1][i] -= d;
           splat[i] = -m_run;
         }
+        l0 *= alpha;
+        l1 *= alpha;
+        if constexpr (MSUM) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) l_acc[i] *= alpha;
+        }
       }
     }
-    // tile t+2 landed (this wave's pieces; t+3's stay in flight), then every wave's
-    if (deep)
+    // tile t+2 landed (this wave's pieces; with 4 slots t+3's stay in flight), then every wave's
+    if (NS == 4 && deep)
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1153,6 +1181,13 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
 
 
   if (!active) return;
+  // the query's row sum: this half-wave's keys + the other half's (same bits in both)
+  float l_sum = l0 + l1;
+  if constexpr (MSUM) l_sum = l_acc[0];
+  else {
+    auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_sum), __float_as_uint(l_sum), false, false);
+    l_sum = __uint_as_float(x[0]) + __uint_as_float(x[1]);
+  }
   if (tail_inline && tail_keys > 0) {  // the 1-key tail of 577 / 1025: exact per-key updates
     const uint16_t* kt_g = base + HDt;
     const uint16_t* vt_g = base + 2 * HDt;
@@ -1170,7 +1205,7 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
       const float mn = fmaxf(m_run, sp);
       const float alpha = __builtin_amdgcn_exp2f(m_run - mn), p = __builtin_amdgcn_exp2f(sp - mn);
       m_run = mn;
-      l_acc[0] = fmaf(l_acc[0], alpha, p);
+      l_sum = fmaf(l_sum, alpha, p);
       const uint16_t* vr = vt_g + (size_t)j * ld;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
@@ -1187,7 +1222,7 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const uint16_t* __restri
   // O[q][d]: the lane holds d = 32 db + 8 k4 + 4 hh + i; the two half-waves' 8-byte pieces
   // of column groups k4, k4 + 1 are exchanged with v_permlane32_swap so every lane stores 16
   // contiguous bytes (half 0: columns 8 k4 .. +7, half 1: 8 (k4 + 1) .. +7)
-  const float inv = 1.0f / l_acc[0];
+  const float inv = 1.0f / l_sum;
   const bool qok = q0 + r < N;
   uint16_t* op = out + ((size_t)b * N + min(q0 + r, N - 1)) * HDt + h * HD_;
 #pragma unroll
@@ -1221,7 +1256,7 @@ void launch_attn(const uint16_t* q, uint16_t* o, int batch, int seq, int heads, 
 }  // namespace
 
 extern "C" int aaclip_set_attn_variant(int variant) {
-  AACLIP_REQUIRE(variant >= 0 && variant <= 5);
+  AACLIP_REQUIRE(variant >= 0 && variant <= 7);
   g_attn_variant = variant;
   return AACLIP_OK;
 }
@@ -1245,12 +1280,15 @@ extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch
     uint8_t* mx = dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr;
     // the 32x32 pipelined kernel: non-causal, a key tail of at most 8 (577 / 1025 tokens),
     // at least one full tile, 16-bit output
-    const bool k32 = v == 5 && !(flags & AACLIP_ATTN_CAUSAL) && seq % KT <= 8 && seq >= KT && !mx;
-    if (k32) {
-      if (dtype == AACLIP_F16)
-        attn32_kernel<true><<<(unsigned)nwg, 256, 0, s>>>(q, o, batch, seq, heads, flags);
-      else
-        attn32_kernel<false><<<(unsigned)nwg, 256, 0, s>>>(q, o, batch, seq, heads, flags);
+    const bool k32 = v >= 5 && !(flags & AACLIP_ATTN_CAUSAL) && seq % KT <= 8 && seq >= KT && !mx;
+    if (k32) {  // 5: 2 WG/CU + MFMA row sums, 6: 2 WG/CU + VALU row sums, 7: 3 WG/CU + VALU row sums
+#define A32(H, OCC, MS) attn32_kernel<H, OCC, MS><<<(unsigned)nwg, 256, 0, s>>>(q, o, batch, seq, heads, flags)
+      if (dtype == AACLIP_F16) {
+        if (v == 5) A32(true, 2, true); else if (v == 6) A32(true, 2, false); else A32(true, 3, false);
+      } else {
+        if (v == 5) A32(false, 2, true); else if (v == 6) A32(false, 2, false); else A32(false, 3, false);
+      }
+#undef A32
     } else if (dtype == AACLIP_F16) {
       if (v == 2) launch_attn<true, 4, 2, 2>(q, o, batch, seq, heads, flags, nullptr, 0, s);
       else if (v == 3) launch_attn<true, 2, 4, ATTN_STAGES, 1>(q, o, batch, seq, heads, flags, nullptr, 0, s);

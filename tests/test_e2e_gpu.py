@@ -17,6 +17,11 @@ from oracle import synth
 
 pytestmark = pytest.mark.gpu
 
+# bf16 patch-label flips against the reference goldens where its margin exceeds 1e-3 (the
+# measured counts, round 4; the tests hold them to twice that)
+BF16_FLIPS_336, BF16_FLIPS_336_LEVEL = 6, (0, 4, 2, 0)
+BF16_FLIPS_518, BF16_FLIPS_518_LEVEL = 4, (1, 2, 1, 0)
+
 
 @pytest.fixture(scope="module")
 def weights(dev):
@@ -74,9 +79,11 @@ def test_visual_bf16_parity(dev, golden, weights):
     print("bf16:", r)
     assert r["map_ok"], r
     # bf16 operands (8 significant bits) can flip a patch label whose margin is within
-    # their rounding: reported, and held to a regression bound (the contract mode,
-    # fp16, has 0: tests/test_fp16_gpu.py)
-    assert r["flips_sure"] <= 0.01 * r["n_sure"], r
+    # their rounding: reported, and held to a regression bound of twice the measured count
+    # (round 4: 6 of 4597 sure labels, per level [0, 4, 2, 0]; the contract mode, fp16,
+    # has 0: tests/test_fp16_gpu.py) -- a kernel change that doubles them fails here
+    assert r["flips_sure"] <= 2 * BF16_FLIPS_336, r
+    assert all(f <= 2 * m + 2 for f, m in zip(r["flips_sure_per_level"], BF16_FLIPS_336_LEVEL)), r
     e = golden["e2e"]
     x = torch.from_numpy(synth.images(111, 2, 336)).to(dev)
     T = torch.from_numpy(e["T"]).to(dev)
@@ -245,8 +252,9 @@ def test_518_default_size_parity(dev, dtype):
     flips = int(fl[sure].sum())
     per_level = [int(fl[:, lv][sure[:, lv]].sum()) for lv in range(fl.shape[1])]
     print(dtype, f"518 patch-label flips (sure) {flips}/{int(sure.sum())} per level {per_level}")
-    if dtype == torch.bfloat16:
-        assert flips <= 0.01 * sure.sum()
+    if dtype == torch.bfloat16:  # measured 4 of 5469 (per level [1, 2, 1, 0]): twice that bounds it
+        assert flips <= 2 * BF16_FLIPS_518, (flips, per_level)
+        assert all(f <= 2 * m + 2 for f, m in zip(per_level, BF16_FLIPS_518_LEVEL)), per_level
     else:
         assert flips == 0
     if dtype == torch.float32:

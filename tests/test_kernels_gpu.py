@@ -383,20 +383,22 @@ def test_attention_spec_equals_split(dev, dt, B, N, H, spikes):
     assert err < (3e-2 if dt == torch.bfloat16 else 4e-3), err
 
 
+@pytest.mark.parametrize("variant", [5, 6, 7])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, False), (1, 1025, 16, False), (2, 72, 4, False),
                                           (1, 64, 2, False), (3, 136, 2, False), (2, 129, 4, False),
                                           (5, 577, 2, False),
                                           # not the 32x32 kernel's shapes: fall back to the 16x16 one
                                           (3, 77, 12, True), (2, 73, 4, False), (2, 5, 2, False)])
-def test_attention_32x32_pipelined(dev, dt, B, N, H, causal):
+def test_attention_32x32_pipelined(dev, variant, dt, B, N, H, causal):
     """Variant 5 (attn32_kernel: v_mfma_f32_32x32x16, S(t+1) = K(t+1).Q^T beside P(t)'s
     exponentials, 3-slot ring) against float64, every tile count parity (odd / even, the
-    loop is unrolled by two), the inline 1..8-key tail, a single tile, query tails."""
+    loop is unrolled by two), the inline 1..8-key tail, a single tile, query tails; 6 / 7 =
+    the same with f32 VALU row sums at 2 / 3 workgroups per CU."""
     torch.manual_seed(B * N + H + 5)
     qkv = (torch.randn(B * N, 3 * H * 64, device=dev) * 1.5).to(dt)
     out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
-    _lib.call("aaclip_set_attn_variant", 5)
+    _lib.call("aaclip_set_attn_variant", variant)
     try:
         ops.attention(qkv, out, B, N, H, causal=causal)
     finally:
@@ -405,8 +407,9 @@ def test_attention_32x32_pipelined(dev, dt, B, N, H, causal):
     assert err < (3e-2 if dt == torch.bfloat16 else 4e-3), err
 
 
+@pytest.mark.parametrize("variant", [5, 6, 7])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_attention_32x32_rescale_paths(dev, dt):
+def test_attention_32x32_rescale_paths(dev, variant, dt):
     """Variant 5 under the deferred-max branch: a slowly rising key norm (deferred, p up to
     256), late spikes at several tiles (the rescale of the pipelined S(t+1), O and l), and
     a NaN-free result equal to float64 within the 16-bit bound; also with q prescaled."""
@@ -425,7 +428,7 @@ def test_attention_32x32_rescale_paths(dev, dt):
         if pre and dt == torch.float16:
             xin = xin.to(dt)
         out = torch.empty(B * N, H * 64, device=dev, dtype=dt)
-        _lib.call("aaclip_set_attn_variant", 5)
+        _lib.call("aaclip_set_attn_variant", variant)
         try:
             ops.attention(xin, out, B, N, H, q_prescaled=pre)
         finally:
