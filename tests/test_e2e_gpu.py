@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 # measured counts, round 4; the tests hold them to twice that)
 BF16_FLIPS_336, BF16_FLIPS_336_LEVEL = 6, (0, 4, 2, 0)
 BF16_FLIPS_518, BF16_FLIPS_518_LEVEL = 4, (1, 2, 1, 0)
+BF16_FLIPS_QUICK = 1  # of 2303 (QuickGELU towers, golden_quick)
 
 
 @pytest.fixture(scope="module")
@@ -333,7 +334,7 @@ def test_quick_gelu_towers_parity(dev, weights, dtype):
     atol, rtol = (1e-3, 1e-2) if dtype != torch.bfloat16 else (3e-3, 1.5e-2)
     assert (err <= atol + rtol * np.abs(q["map_ind_sub"])).all()
     np.testing.assert_allclose(score.cpu().numpy(), q["score"], atol=1e-3)
-    assert flips <= (0 if dtype != torch.bfloat16 else 0.01 * sure.sum())
+    assert flips <= (0 if dtype != torch.bfloat16 else 2 * max(1, BF16_FLIPS_QUICK))
     # the erf-GELU engine on the same weights is visibly off this golden (in bf16 the
     # activation swap moves the map by 1.5e-2 against bf16's own 5e-3: a factor 2.5 there)
     plain = _visual(weights, dtype).predict(x, T, "Industrial")[0].cpu().numpy()[:, ::7, ::7]
