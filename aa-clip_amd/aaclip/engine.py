@@ -422,8 +422,15 @@ class VisualEngine:
         ops.image_score(det_raw, out_map.shape[0], ws["P"], ws["partial"], det=ws["det"], T=T, score=out_score)
 
     def _chunk_streams(self, n: int):
-        if len(getattr(self, "_streams", [])) < n:
-            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(n)]
+        # stream_prio (A/B): the first chunk's stream at high priority, so the dispatcher
+        # serves its workgroups first and the chunks drift apart (one chunk's tile-starved
+        # launches then share the CUs with the other's row kernels and wide GEMMs)
+        prio = int(getattr(self, "stream_prio", 0))
+        key = (n, prio)
+        if getattr(self, "_streams_key", None) != key:
+            self._streams = [torch.cuda.Stream(device=self.device, priority=(-1 if (prio and i == 0) else 0))
+                             for i in range(n)]
+            self._streams_key = key
         return self._streams[:n]
 
     @torch.no_grad()
