@@ -174,6 +174,7 @@ class VisualEngine:
         # aaclip_anomaly_map_partials) instead of segbuf rows + a stream over them;
         # AACLIP_MAP_PARTIALS=0 restores the row path (A/B)
         self.map_partials = os.environ.get("AACLIP_MAP_PARTIALS", "1") == "1"
+        self.stream_prio = 0  # A/B: 1 = the first chunk stream at high priority (_chunk_streams)
 
     # ------------------------------------------------------------------ workspace
     def _workspace(self, B: int, S: int, slot: int = 0):
