@@ -14,7 +14,8 @@ Data layout in HBM (token-major "NLD", one row per token):
   xb     bf16 [B*(P+1), 1024]   bf16 copy of x written by the c_proj epilogue (adapter input)
   u      fp32 [B*(P+1), 1024]   LeakyReLU(adapter(x))
   tap_l  cdt  [B*P, 1024]       ln_post(x[:, 1:]) at each level
-  seg    fp32 [B*P, (L+1)*768]  seg_proj of level l in cols l*768.., det_proj in cols L*768..
+  seg    fp32 [B*P, (L+1)*768]  seg_proj of level l in cols l*768.., det_proj in cols L*768.. (forward())
+  spart  fp32 [B*P, (L+1)*96]   predict(), 16-bit modes: per (row, level, 32 columns) {|v|^2, v.t0, v.t1, 0}
 cdt = compute dtype: bf16 (MFMA bf16, perf path) or fp32 (fp32 MFMA, parity mode).
 Weights are packed once: nn.Linear [N,K] layout kept (the GEMM is A.W^T);
 conv1 flattened to [1024, 640] (K padded 588 -> 640 with zeros).
