@@ -923,43 +923,52 @@ __global__ __launch_bounds__(256, OCC) void attn32_kernel(const uint16_t* __rest
       for (int e = 0; e < 8; ++e) qf[ks][e] = (E)((float)qf[ks][e] * sl2);
   }
 
-  // K/V DMA: wave w moves 8-row pieces w and w+4 of the K and of the V tile (lane-linear
-  // image; chunk (lane&7) of a row holds logical chunk (lane&7) ^ (row&7): swz())
+  // K/V DMA: wave w moves 8-row pieces w and w+4 of the K and of the V tile into a
+  // lane-linear image whose physical 16-B chunk p of row `row` holds logical chunk
+  // p ^ kswz(row) (K) / p ^ vswz(row) (V). The 32x32 operand reads need their own XORs
+  // (the 16x16 kernel's row & 7 is 2-way conflicted here, PMC: 5.9 M conflict cycles):
+  // K's ds_read_b128 lane groups ({0-3,12-15,20-27}, ...: rows r of one parity, one
+  // logical chunk) hit distinct banks with (row >> 1) & 7; V's transposed reads (a
+  // 32-lane half: 4 consecutive rows x 4 chunks x 2 halves) with bit 2 flipped on rows
+  // 2, 3 mod 4.
   const int64_t head0 = (int64_t)b * N * ld + h * HD_;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(qkv + head0), 0,
                                                     (int)(((int64_t)batch * N * ld - head0) * 2), 0x00020000);
-  int voff[2];
+  auto kswz = [](int row) { return (row >> 1) & 7; };
+  auto vswz = [](int row) { return ((row >> 1) & 1) << 2; };
+  int koff[2], voff[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (i * 4 + wid) * 8 + (lane >> 3);
-    voff[i] = (int)(row * ld + HDt + ((lane & 7) ^ (row & 7)) * 8) * 2;
+    koff[i] = (int)(row * ld + HDt + ((lane & 7) ^ kswz(row)) * 8) * 2;
+    voff[i] = (int)(row * ld + 2 * HDt + ((lane & 7) ^ vswz(row)) * 8) * 2;
   }
-  const int row_bytes = (int)ld * 2, v_off = HDt * 2;
+  const int row_bytes = (int)ld * 2;
   auto stage = [&](int t, int slot) {
     char* kb = smem + slot * SLOT;
     const int so = t * KT * row_bytes;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(kb + (i * 4 + wid) * 1024), 16, voff[i], so, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(kb + KT * 128 + (i * 4 + wid) * 1024), 16, voff[i],
-                                               so + v_off, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(kb + (i * 4 + wid) * 1024), 16, koff[i], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(kb + KT * 128 + (i * 4 + wid) * 1024), 16, voff[i], so,
+                                               0, 0);
     }
   };
   // per-lane LDS read addresses (slot 0; + slot * SLOT per tile):
-  // K frag (kb, ks): row 32 kb + r, chunk 2 ks + hh -> swz; kb = 1 is +4096 (same XOR)
+  // K frag (kb, ks): row 32 kb + r, logical chunk 2 ks + hh; kb = 1 is +4096 (same XOR)
   const uint32_t lds0 = lds_addr(smem);
   uint32_t ka[4];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) ka[ks] = lds0 + swz(r, 2 * ks + hh);
+  for (int ks = 0; ks < 4; ++ks) ka[ks] = lds0 + r * 128 + (((2 * ks + hh) ^ kswz(r)) << 4);
   // V^T frag: 16-lane group G = lane >> 4 reads 4 rows row0 + (lane & 15) / 4 of columns
-  // 32 db + 16 (G & 1) + 4 (lane & 3) .. +3; row0 = 32 kb + 16 st + 8 j4 + 4 hh, so the
-  // row's XOR term (4 hh + qq) & 7 is the same for every (kb, st, j4): those are immediates
+  // 32 db + 16 (G & 1) + 4 (lane & 3) .. +3; row0 = 32 kb + 16 st + 8 j4 + 4 hh = 0 mod 4, so
+  // the row's XOR term vswz(row0 + qq) is the same for every (kb, st, j4): immediates
   const int qq = (lane & 15) >> 2, gcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
   uint32_t va[2];
 #pragma unroll
   for (int db = 0; db < 2; ++db) {
     const int row = 4 * hh + qq, col = 32 * db + gcol;
-    va[db] = lds0 + KT * 128 + swz(row, col >> 3) + (col & 7) * 2;
+    va[db] = lds0 + KT * 128 + row * 128 + (((col >> 3) ^ vswz(row)) << 4) + (col & 7) * 2;
   }
 
   const int tail_keys = N % KT;
