@@ -176,6 +176,7 @@ class VisualEngine:
         # AACLIP_MAP_PARTIALS=0 restores the row path (A/B)
         self.map_partials = os.environ.get("AACLIP_MAP_PARTIALS", "1") == "1"
         self.stream_prio = 0  # A/B: 1 = the first chunk stream at high priority (_chunk_streams)
+        self.stagger = 0  # A/B: chunk 1 waits for chunk 0's first `stagger` block sub-ops (predict)
 
     # ------------------------------------------------------------------ workspace
     def _workspace(self, B: int, S: int, slot: int = 0):
@@ -271,11 +272,13 @@ class VisualEngine:
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
     @_on_device
-    def forward_raw(self, x: torch.Tensor, slot: int = 0, T: torch.Tensor | None = None):
+    def forward_raw(self, x: torch.Tensor, slot: int = 0, T: torch.Tensor | None = None, mark=None):
         """Run the visual tower; returns (seg_raw list of [B*P, 768] views,
         det_raw [B*P, 768] view, workspace). Rows are unnormalised projections.
         With T (predict, 16-bit modes) the projections are written as anomaly-map
-        partials against T into ws["spart"] instead, and (None, None, ws) is returned."""
+        partials against T into ws["spart"] instead, and (None, None, ws) is returned.
+        mark = (k, event): record `event` on the current stream after block sub-op k
+        (4 per block: qkv, attention, out-proj, MLP) -- the chunk stagger of predict()."""
         if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != x.shape[3] or x.shape[2] % PATCH:
             raise ValueError("input must be [B, 3, S, S] with S a multiple of 14")
         x = x.to(self.device, torch.float32).contiguous()
@@ -343,13 +346,21 @@ class VisualEngine:
                 ln2(blk, H)
                 ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=self.act)
                 ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=aux)
+        def tick(k):
+            if mark is not None and mark[0] == k:
+                mark[1].record(torch.cuda.current_stream(self.device))
+
         for i in range(last):
             blk = self.blocks[i]
             qkv(blk)
+            tick(4 * i)
             attend()
+            tick(4 * i + 1)
             out_proj(blk)
+            tick(4 * i + 2)
             adapt = i < self.adapt_until
             mlp(blk, ws["xb"] if (adapt and ws["xb"] is not None) else None)
+            tick(4 * i + 3)
             tap = ws["taps"][lvl[i + 1]] if (i + 1) in lvl else None
             nxt = self.blocks[i + 1]["ln1"] if i + 1 < last else None
             u = None
@@ -502,13 +513,19 @@ class VisualEngine:
         # images per chunk): whole two-stream C2 step 2240 -> 2295 images/s bf16 (2164 ->
         # 2220 fp16); a single stream keeps the heuristic (1895 vs 2050). Thread-local
         # (aaclip_gemm_concurrent), chosen at launch, so graph capture keeps it.
+        # stagger (A/B): chunk 1 starts after chunk 0 has enqueued `stagger` block sub-ops
+        stag = int(getattr(self, "stagger", 0)) if nstreams > 1 else 0
+        sev = torch.cuda.Event() if stag else None
         with ops.concurrent_gemms(nstreams > 1 and self.dtype in (torch.bfloat16, torch.float16)):
             for i in range(len(sizes)):
                 b0, b1 = bounds[i], bounds[i + 1]
                 st = sts[i % nstreams]
+                if stag and i == 1:
+                    st.wait_event(sev)
                 with torch.cuda.stream(st):
                     seg_raw, det_raw, ws = self.forward_raw(x[b0:b1], slot=_slot0 + i % nstreams,
-                                                            T=T if self.map_partials else None)
+                                                            T=T if self.map_partials else None,
+                                                            mark=(stag, sev) if (stag and i == 0) else None)
                     self._tail(seg_raw, det_raw, ws, T, out_map[b0:b1], out_score[b0:b1], k, s)
         for st, ev in zip(sts, done):
             ev.record(st)
