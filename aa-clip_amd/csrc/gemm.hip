@@ -653,7 +653,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
 // ones: the four phases of tile t+1's first K-step wait vmcnt(8 + S) (S counted per
 // epilogue case; 0 = strict for edge tiles and the run-time-flag epilogues), so the
 // stores drain under four MFMA phases before vmcnt(8) requires them.
-template <bool H16, bool PERSIST>
+// SCORES: the instantiation for aaclip_gemm_scores (OUTM 3 epilogue only), so the
+// anomaly-map partials path adds no registers to the block-GEMM instantiations.
+template <bool H16, bool PERSIST, bool SCORES = false>
 __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   using V8 = h16x8_t<H16>;
   constexpr int BM = 256, BN = 256, TM = 128, TN = 64, RM = 8, RN = 4;
@@ -771,6 +773,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   const bool bf16_out = a.out_dtype != AACLIP_F32;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
   int s_prev = 0;  // stores the previous tile's epilogue left in the vmcnt stream (0 = none / unknown)
+  // diagnostic stamps (variant bit 11, non-persistent launches): shader-clock s_memtime at
+  // kernel start, main-loop end, epilogue issued, epilogue stores complete -> a.aux
+  const bool stamp = !PERSIST && (a.dbg & 4);
+  uint64_t ts[4] = {0, 0, 0, 0};
+  if (stamp) ts[0] = __builtin_amdgcn_s_memtime();
   for (;;) {
     const int m0 = tm * BM, n0 = tn * BN;
     int tm_n = 0, tn_n = 0;
@@ -815,12 +822,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
     // the bias / residual loads only add to it). Edge tiles skip whole row groups: 0.
     const bool full = m0 + BM <= a.M;
     s_prev = 0;
+    if (stamp) ts[1] = __builtin_amdgcn_s_memtime();
     if (a.dbg & 1) {
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
-    } else if (a.out_dtype == kOutScores) {  // seg/det proj -> map partials (no stores to overlap)
+    } else if constexpr (SCORES) {  // seg/det proj -> map partials (no stores to overlap)
       if (key == AACLIP_EPI_LEAKY)
         wave_epilogue<RM, RN, 3, AACLIP_EPI_LEAKY, 0, H16>(a, acc, mw, nw, lane);
       else
@@ -836,7 +844,6 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU, RM * RN / 2)
       EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID, RM * RN)
       EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16, RM * RN + RM * RN / 2)
-      EPI_CASE(false, AACLIP_EPI_BIAS, RM * RN)  // out-proj, deferred residual
       EPI_CASE(false, AACLIP_EPI_LEAKY, RM * RN)
 #undef EPI_CASE
       if (bf16_out)
@@ -853,7 +860,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
     w_vo = w_vo_next;
   }
 #undef PH_SYNC_MFMA
+  if (stamp) ts[2] = __builtin_amdgcn_s_memtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phantom loads drained before exit
+  if (stamp) {
+    ts[3] = __builtin_amdgcn_s_memtime();
+    if (lane < 4) ((uint64_t*)a.aux)[((size_t)blockIdx.x * 8 + wid) * 4 + lane] = ts[lane];
+  }
 }
 
 // ============================ 8-phase ping-pong fp8 MX kernel (256x256, K-step 128)
@@ -1165,7 +1177,7 @@ int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
 
 int cu_count();
 
-template <bool H16, bool PERSIST = false>
+template <bool H16, bool PERSIST = false, bool SCORES = false>
 int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   if (a.N % 256 || a.K % 64) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, 256);
@@ -1177,8 +1189,9 @@ int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   if (PERSIST && !((a.K / 64) % 2 == 0 && tiles > cus && cus > 0)) return launch_bf16_8ph<H16, false>(a, s);
   const size_t lds = 2 * 4 * 128 * 128;
   static unsigned attr_dev = 0;
-  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, PERSIST>, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
-  gemm_bf16_8ph_kernel<H16, PERSIST><<<PERSIST ? cus : tiles, 512, lds, s>>>(a);
+  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, PERSIST, SCORES>, (int)lds, attr_dev))
+    return AACLIP_ERR_LAUNCH;
+  gemm_bf16_8ph_kernel<H16, PERSIST, SCORES><<<PERSIST ? cus : tiles, 512, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -1391,11 +1404,13 @@ extern "C" int aaclip_set_gemm_variant(int variant) {
   // 11 = 64x64); bits 4-7: tile-order
   // group height (0 = 4); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 2048 || fam > 11 || fam == 7) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 4096 || fam > 11 || fam == 7) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 4;
   g_setprio = (variant >> 8) & 1;
-  g_dbg = (variant >> 9) & 3;  // bit 9 skip epilogue, bit 10 skip the global stores
+  // bit 9 skip epilogue, bit 10 skip the global stores, bit 11 the 8-phase kernel's
+  // per-wave s_memtime stamps into the aux pointer (bf16 / fp32 epilogues without aux only)
+  g_dbg = (variant >> 9) & 7;
   return AACLIP_OK;
 }
 
@@ -1464,7 +1479,7 @@ extern "C" int aaclip_gemm_scores(int in_dtype, int M, int N, int K, const void*
       return h16 ? launch_bf16<256, 128, 4, 2, 0, true>(a, s) : launch_bf16<256, 128, 4, 2, 0, false>(a, s);
     default:
       if (!fits) return h16 ? launch_bf16<320, 256, 2, 4, 0, true>(a, s) : launch_bf16<320, 256, 2, 4, 0, false>(a, s);
-      return h16 ? launch_bf16_8ph<true>(a, s) : launch_bf16_8ph<false>(a, s);
+      return h16 ? launch_bf16_8ph<true, false, true>(a, s) : launch_bf16_8ph<false, false, true>(a, s);
   }
 }
 

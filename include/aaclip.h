@@ -156,7 +156,10 @@ int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int
  * fp8 MX GEMM: 0 = 8-phase ping-pong (default), 6 = the 256x256 LDS-DMA kernel; bits 4-7:
  * tile-order group height (0 = 4); bit 8: s_setprio around the MFMA cluster;
  * bit 9: diagnostic timing mode that skips the epilogue (outputs NOT written);
- * bit 10: diagnostic mode that runs the epilogue but skips its global stores.
+ * bit 10: diagnostic mode that runs the epilogue but skips its global stores;
+ * bit 11: the 8-phase kernel writes 4 s_memtime stamps per wave (start, main loop
+ * done, epilogue issued, stores complete) as uint64 to aaclip_gemm's aux pointer,
+ * [tile][wave][4] (only for epilogues without AACLIP_EPI_AUX_BF16).
  * Process-global; not for production use.
  */
 int aaclip_set_gemm_variant(int variant);
