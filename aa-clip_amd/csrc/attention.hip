@@ -647,19 +647,28 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
     }
     return;
   }
+  // 16-B stores: lane group g holds columns 4g..4g+3 of each 16-column block db; a
+  // v_permlane16_swap per packed dword pairs blocks (2p, 2p+1) across groups g, g^1, so
+  // group g ends with 8 consecutive columns: block 2p + (g & 1), columns 8 (g >> 1) .. +7
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) {
     const float inv = 1.0f / l_acc[qb][0];
     const int q = q0 + qb * 16 + c;
-    if (q < N) {
-      uint16_t* o = out + ((size_t)b * N + q) * HDt + h * HD_;
+    uint4 w[2];
 #pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        uint2 r;
-        r.x = pack_h16x2<H16>(ot[qb][db][0] * inv, ot[qb][db][1] * inv);
-        r.y = pack_h16x2<H16>(ot[qb][db][2] * inv, ot[qb][db][3] * inv);
-        *(uint2*)(o + db * 16 + 4 * g) = r;
-      }
+    for (int pr = 0; pr < 2; ++pr) {
+      const uint32_t a0 = pack_h16x2<H16>(ot[qb][2 * pr][0] * inv, ot[qb][2 * pr][1] * inv);
+      const uint32_t a1 = pack_h16x2<H16>(ot[qb][2 * pr][2] * inv, ot[qb][2 * pr][3] * inv);
+      const uint32_t b0 = pack_h16x2<H16>(ot[qb][2 * pr + 1][0] * inv, ot[qb][2 * pr + 1][1] * inv);
+      const uint32_t b1 = pack_h16x2<H16>(ot[qb][2 * pr + 1][2] * inv, ot[qb][2 * pr + 1][3] * inv);
+      const auto x = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+      const auto y = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+      w[pr] = uint4{x[0], y[0], x[1], y[1]};
+    }
+    if (q < N) {
+      uint16_t* o = out + ((size_t)b * N + q) * HDt + h * HD_ + 16 * (g & 1) + 8 * (g >> 1);
+      *(uint4*)(o) = w[0];
+      *(uint4*)(o + 32) = w[1];
     }
   }
 }

@@ -219,7 +219,7 @@ __device__ __forceinline__ uint4 pair_h16(const float4_t& lo, const float4_t& hi
 // H16: the 16-bit storage of OUTM 1 and of the aux copy is fp16 (else bf16).
 template <int RM, int RN, int OUTM, int EPI, int SCALED, bool H16 = false, int PD = 2>
 __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
-                                              int lane) {
+                                              int lane, const float* lbias = nullptr) {
   static_assert(RN % 2 == 0, "column tiles are paired");
   static_assert(OUTM != 2 || RN == 4, "fp8 MX output: one 64-column block per wave");
   static_assert(OUTM != 3 || RN == 2 || RN == 4, "score partials: one or two 32-column groups per wave");
@@ -231,8 +231,9 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
   const int pcol = nw + 16 * (fq & 1) + 8 * (fq >> 1);  // paired bf16 layout
   float4_t bias[RN];
 #pragma unroll
-  for (int j = 0; j < RN; ++j)
-    bias[j] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)(a.bias + ncol + 16 * j) : float4_t{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < RN; ++j)  // lbias: the tile's bias staged in LDS by the kernel (indexed by column)
+    bias[j] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)((lbias ? lbias : a.bias) + ncol + 16 * j)
+                                      : float4_t{0.f, 0.f, 0.f, 0.f};
   // OUTM 3 (score partials): this lane's anchor values, t0 / t1 of columns ncol + 16 j + e
   float4_t ta0[RN], ta1[RN];
   if constexpr (OUTM == 3) {
@@ -715,6 +716,14 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   float4_t acc[RM][RN];
   V8 af[4][2], bfr[2][2][2];  // A sub-block (4 tiles x kk), B sub-blocks [q][j][kk]
 
+  // the tile's 256 bias values into LDS behind the ring (one 1-KiB DMA by wave 0, retired by
+  // the prologue's vmcnt(8) as the oldest op): the epilogue reads them from LDS instead of
+  // waiting out a global-load round trip at its start
+  const bool lds_bias = !PERSIST && !SCORES && (a.epi & AACLIP_EPI_BIAS);
+  if (lds_bias && wid == 0) {
+    const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)a.bias, 0, (int)((uint32_t)a.N * 4u), 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, LDS_PTR(smem + 2 * STAGE), 16, (tn * BN + 4 * lane) * 4, 0, 0, 0);
+  }
   // prologue: all of K-step 0, then A0 / B0 of K-step 1 (the steady state's P3/P4 of K-step -1)
   issue(0, 0);
   issue(2, 0);
@@ -817,6 +826,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
     // row 1 re-takes its one-barrier lag before the next tile
     if (wr == 0) __builtin_amdgcn_s_barrier();
     const int mw = m0 + wr * TM, nw = n0 + wc * TN;
+    const float* lbp = (const float*)(smem + 2 * STAGE) - n0;  // staged bias, by column
+    const float* lb = lds_bias ? lbp : nullptr;
     // S for the next tile's first K-step: a LOWER bound on the VMEM ops this epilogue
     // issues between the next tile's prefetched regions and its own next DMA (stores;
     // the bias / residual loads only add to it). Edge tiles skip whole row groups: 0.
@@ -836,7 +847,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
     } else {
 #define EPI_CASE(BF, E, NS)                                               \
   if (bf16_out == (BF) && key == (E)) {                                   \
-    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane);   \
+    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane,    \
+                                                 (!PERSIST && ((E) & AACLIP_EPI_BIAS)) ? lbp : nullptr); \
     s_prev = full && !(a.dbg & 2) ? (NS) : 0;                             \
   } else
       EPI_CASE(true, AACLIP_EPI_BIAS, RM * RN / 2)
@@ -847,9 +859,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       EPI_CASE(false, AACLIP_EPI_LEAKY, RM * RN)
 #undef EPI_CASE
       if (bf16_out)
-        wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane);
+        wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane, lb);
       else
-        wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane);
+        wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane, lb);
     }
     if (!PERSIST || !has_next) break;
     if (wr == 1) __builtin_amdgcn_s_barrier();
@@ -1187,7 +1199,7 @@ int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   // the K-step stream across tiles needs an even K-step count (stage = kt & 1)
   const int cus = cu_count() & ~7;
   if (PERSIST && !((a.K / 64) % 2 == 0 && tiles > cus && cus > 0)) return launch_bf16_8ph<H16, false>(a, s);
-  const size_t lds = 2 * 4 * 128 * 128;
+  const size_t lds = 2 * 4 * 128 * 128 + 1024;  // the ring + the tile's bias
   static unsigned attr_dev = 0;
   if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, PERSIST, SCORES>, (int)lds, attr_dev))
     return AACLIP_ERR_LAUNCH;
