@@ -155,7 +155,8 @@ def test_gemm_families_bit_identical(dev, dt, M, N, K):
     MFMA k-slices, ascending, one fp32 accumulator per output), so their outputs are
     bit-identical -- the engine may pick any family per shape, stream count and batch
     without changing an image's bits. Covers the K-step-32 two-workgroup kernel against
-    the 8-phase, 320x256, 128x128 and 64x64 ones (bf16 out with bias, fp32 out with residual)."""
+    the 8-phase, 320x256, 128x128 and 64x64 ones (bf16 out with bias, fp32 out with residual,
+    fp32 out with residual + 16-bit aux copy: the 8-phase kernel's LDS-staged residual epilogue)."""
     g = torch.Generator(device=dev).manual_seed(M + K)
     a = torch.randn(M, K, device=dev, generator=g).to(dt)
     w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
@@ -170,12 +171,21 @@ def test_gemm_families_bit_identical(dev, dt, M, N, K):
             ops.gemm(a, w, o16, bias=bias)
             o32 = res.clone()
             ops.gemm(a, w, o32, bias=bias, residual=o32)
+            x32 = res.clone()
+            xaux = torch.empty(M, N, device=dev, dtype=dt)
+            ops.gemm(a, w, x32, bias=bias, residual=x32, aux=xaux)
         finally:
             _lib.call("aaclip_set_gemm_variant", 0)
-        outs.append((o16, o32))
-    for f, (o16, o32) in zip(fams[1:], outs[1:]):
+        outs.append((o16, o32, x32, xaux))
+    ref = (a.double() @ w.double().T + bias.double()) + res.double()
+    assert ((outs[0][1].double() - ref).abs() <= 2e-2 * ref.abs() + 2e-2).all()
+    assert torch.equal(outs[0][2], outs[0][1])
+    assert torch.equal(outs[0][3], outs[0][1].to(dt))
+    for f, (o16, o32, x32, xaux) in zip(fams[1:], outs[1:]):
         assert torch.equal(o16.view(torch.int16), outs[0][0].view(torch.int16)), f
         assert torch.equal(o32, outs[0][1]), f
+        assert torch.equal(x32, outs[0][2]), f
+        assert torch.equal(xaux.view(torch.int16), outs[0][3].view(torch.int16)), f
 
 
 def test_gemm_bf16_asymmetric_identity(dev):
