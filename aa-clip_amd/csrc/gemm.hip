@@ -734,9 +734,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0(0), B0(0) landed
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: wave row 1 runs one barrier behind
+  // No s_setprio flips around the MFMA clusters (the sched_barrier fences already pin each
+  // cluster between its barriers): C2 step +0.8 % over setprio 1/0 around every cluster;
+  // a static prio 1 for the younger wave row measured the same as none, keeping the flips
+  // for the older row -2.5 % (profiles/r04/gemm_8ph_priority_ab.txt)
 
   auto mfma_q = [&](int qa, int qb) {
-    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -744,7 +747,6 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[qa * 4 + i][qb * 2 + j] = mfma16(bfr[qb][j][kk], af[i][kk], acc[qa * 4 + i][qb * 2 + j]);
-    __builtin_amdgcn_s_setprio(0);
   };
   auto read_a = [&](const char* st, int q) {
 #pragma unroll
