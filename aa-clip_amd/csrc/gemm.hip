@@ -786,7 +786,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   int s_prev = 0;  // stores the previous tile's epilogue left in the vmcnt stream (0 = none / unknown)
   // diagnostic stamps (variant bit 11, non-persistent launches): shader-clock s_memtime at
   // kernel start, main-loop end, epilogue issued, epilogue stores complete -> a.aux
-  const bool stamp = !PERSIST && (a.dbg & 4);
+  const bool stamp = !PERSIST && (a.dbg & 4) && a.aux && !(a.epi & AACLIP_EPI_AUX_BF16);
   uint64_t ts[4] = {0, 0, 0, 0};
   if (stamp) ts[0] = __builtin_amdgcn_s_memtime();
   for (;;) {
