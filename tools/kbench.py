@@ -155,6 +155,13 @@ def main():
         amap = torch.empty(B, S, S, device=dev)  # both stages: patch scores + blur/upsample
         ms = timeit(lambda: ops.anomaly_map(levels, T, amap, grid, g=24, ksize=7, sigma=1.0), args.reps)
         res["anomaly_map"] = (ms, (4 * P * 768 * 4 + B * S * S * 4) / ms / 1e6)
+        # the predict() form since round 4: map + image score from the projection GEMMs'
+        # per-(row, 32-column) partials (4 levels + det, 24 groups of {||v||^2, v.t0, v.t1, 0})
+        part = torch.rand(P, 5 * 4 * ops.SCORE_GROUPS, device=dev, generator=g) + 0.5
+        det_ws, score = torch.empty(P, device=dev), torch.empty(B, device=dev)
+        ms = timeit(lambda: ops.anomaly_map_partials(part, 4, amap, grid, g=24, ksize=7, sigma=1.0, det_ws=det_ws,
+                                                     score=score), args.reps)
+        res["anomaly_map_partials"] = (ms, (part.numel() * 4 + B * S * S * 4 + 2 * P * 4) / ms / 1e6)
     if args.only == "prep":  # device preprocessing: B decoded 1024x1024 RGB -> fp32 [B,3,S,S] (+ masks)
         from aaclip.preprocess import Preprocessor
         S = 336 if args.tokens == 577 else 448
@@ -173,7 +180,7 @@ def main():
         ms = timeit(lambda: ops.layernorm(x, lw, lb, h), args.reps)
         res["layernorm"] = (ms, (R * W * 6) / ms / 1e6)
     for k, (ms, rate) in res.items():
-        unit = "GB/s" if k in ("layernorm", "patch_scores", "anomaly_map") or k.endswith("quantA") or k[:4] in ("prep", "mask") \
+        unit = "GB/s" if k in ("layernorm", "patch_scores", "anomaly_map", "anomaly_map_partials") or k.endswith("quantA") or k[:4] in ("prep", "mask") \
             else "TFLOP/s"
         print(f"{k:10s} {ms * 1e3:9.1f} us  {rate:8.1f} {unit}")
 

@@ -51,8 +51,13 @@ if __name__ == "__main__":
         # 320x256 kernel (58 x 12 / 58 x 16 tiles) or the 8-phase 256x256 one (73 x 12 / 73 x 16)
         grids = {696 * 512, 928 * 512, 876 * 512, 1168 * 512}
         gemm = [e for e in s if "gemm_bf16" in e["kernel"] and e["grid_size"] in grids and "hbm_bytes" in e]
-        mp = [e for e in s if "patch_scores" in e["kernel"] and "hbm_bytes" in e]
-        bu = [e for e in s if "blur_upsample" in e["kernel"] and "hbm_bytes" in e]
+        # the map as predict() runs it since round 4: partial_scores + blur_upsample_score
+        # (the row form, patch_scores + blur_upsample, when a summary holds only that)
+        mp = [e for e in s if "partial_scores" in e["kernel"] and "hbm_bytes" in e]
+        bu = [e for e in s if "blur_upsample_score" in e["kernel"] and "hbm_bytes" in e]
+        if not mp:
+            mp = [e for e in s if "patch_scores" in e["kernel"] and "hbm_bytes" in e]
+            bu = [e for e in s if "blur_upsample" in e["kernel"] and "hbm_bytes" in e]
         t = {"source": f"rocprofv3 --pmc passes (tools/prof_pmc.sh) summarised by tools/pmc_summary.py from {a.root}; "
                        "read = FETCH_SIZE*1024*2 (gfx950 half-count correction), write = WRITE_SIZE*1024"}
         if gemm:
