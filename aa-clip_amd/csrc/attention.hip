@@ -411,7 +411,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
   static_assert(NS == 2 || NS == 3, "ATTN_STAGES must be 2 or 3");
   using V8 = h16x8_t<H16>;
   using E = h16_t<H16>;
-  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * KT * 128];  // [stage][K|V][64][128B]
+  // [stage][K|V][64][128B], then the key tail's K and V rows ([K|V][8][128B])
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * KT * 128 + 2048];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, c = lane & 15;
@@ -506,6 +507,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
   // Ring of NS K/V stages: tile t+NS-1 is issued while tile t is computed; the
   // end-of-tile wait is COUNTED (vmcnt retires in order, 4 DMAs per wave per
   // stage) so tiles t+2.. stay in flight across the barrier.
+  // the key tail's K / V rows (<= 8) into LDS behind the ring, by wave 0 ahead of the
+  // first stage (the oldest ops: the prologue's counted wait retires them), so the fold
+  // after the tile loop reads LDS instead of waiting out a global-load round trip
+  char* const tail_lds = smem + NS * 2 * KT * 128;
+  if (tail_inline && wid == 0) {
+    const int tvo = ((N - tail_keys + (lane >> 3)) * (int)ld + HDt + (lane & 7) * 8) * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(tail_lds), 16, tvo, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(tail_lds + 1024), 16, tvo, v_off, 0, 0);
+  }
   stage(0, 0);
   if (NS > 2 && ntiles > 1) stage(1, 1);
   wait_barrier<2 * PR>(NS > 2 && ntiles > 1);
@@ -559,16 +569,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
   if (ntiles == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prologue's tile-0 DMA
 
   if (tail_inline && active) {
-    const uint16_t* kt_g = base + HDt;
-    const uint16_t* vt_g = base + 2 * HDt;
     for (int j = N - tail_keys; j < N; ++j) {
-      const uint16_t* kr = kt_g + (size_t)j * ld;
-      const uint16_t* vr = vt_g + (size_t)j * ld;
-      const V8 k0 = *(const V8*)(kr + 8 * g), k1 = *(const V8*)(kr + 32 + 8 * g);
+      const char* kr = tail_lds + (j - (N - tail_keys)) * 128;  // K row j (LDS), V row j at +1024
+      const V8 k0 = *(const V8*)(kr + 16 * g), k1 = *(const V8*)(kr + 64 + 16 * g);
       float vv[4][4];  // V[j][d = db*16 + 4g + i], the lane's O columns
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
-        const uint2 w = *(const uint2*)(vr + db * 16 + 4 * g);
+        const uint2 w = *(const uint2*)(kr + 1024 + db * 32 + 8 * g);
         vv[db][0] = h16_to_f32<H16>((uint16_t)(w.x & 0xffff));
         vv[db][1] = h16_to_f32<H16>((uint16_t)(w.x >> 16));
         vv[db][2] = h16_to_f32<H16>((uint16_t)(w.y & 0xffff));
