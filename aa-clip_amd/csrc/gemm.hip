@@ -192,9 +192,10 @@ __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, i
 // e = 0..3 -- one row, 4 consecutive columns. fp32 rows leave as one 16-B store per
 // (i, j); bf16 rows are packed to 8 B and paired across column tiles j, j+1 with
 // v_permlane16_swap (lanes fq even/odd exchange halves) into 16-B stores. No LDS
-// round trip and no lgkmcnt waits: the measured LDS-staged form spent more time
-// staging than storing. The residual rows of tile-row i+1 are loaded before tile-row
-// i's stores (vmcnt retires in issue order).
+// round trip (round 1 measured an LDS-staged form slower on the 320-row kernel); the
+// 8-phase kernel does go through LDS (wave_epilogue_lds) to coalesce its accesses.
+// The residual rows of tile-row i+1 are loaded before tile-row i's stores (vmcnt
+// retires in issue order).
 constexpr int EPI_REMAP = 64;
 
 template <bool H16>
@@ -362,6 +363,124 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
       if (epi & AACLIP_EPI_AUX_BF16) {
 #pragma unroll
         for (int q = 0; q < RN / 2; ++q) *(uint4*)((uint16_t*)a.aux + orow * a.ldaux + pcol + 32 * q) = pk[q];
+      }
+    }
+  }
+}
+
+// The 8-phase kernel's epilogue (OUTM 0 / 1, one wave's 128 x 64 tile): the same
+// arithmetic as wave_epilogue, but every global access is quad-coalesced. In the
+// accumulator layout consecutive lanes hold consecutive ROWS, so each 4-lane quad of a
+// 16-B store or load touches 4 rows; the per-CU address path handles such an
+// instruction at a third of the rate of one whose quads each cover 64 contiguous bytes
+// (tools/atomic_bench.hip: 16-B stores 6.0k vs 2.0k cycles per 128 KiB, load + store
+// 13.1k vs 5.6k, with 32 CUs busy). Each 16-row group goes through a per-wave LDS slot
+// (written in the accumulator layout, read back with lane L on row L/4, 16-B chunk
+// L%4 + 4k), XOR-swizzled so both sides are bank-conflict free; the residual is loaded,
+// added and stored in the read-back layout (same fp32 adds, so the same bits). A
+// wave's LDS operations execute in order, so the slot is reused without waits between
+// groups.
+// fp32 rows: 16 chunks of 16 B, chunk c of row r at c ^ f(r), f(r) = (r & 3) << 2 | r >> 2;
+// 16-bit rows: 8 chunks, slot 8r + (c ^ g(r)), g(r) = ((r >> 1) & 1) << 2 | (r >> 2) & 3
+// (16-bit rows with a residual take the fp32 form and store 8 B per lane).
+template <int RM, int RN, int OUTM, int EPI, bool H16, int PD = 2>
+__device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
+                                                  int lane, const float* lbias, char* slot) {
+  static_assert(RN == 4 && (OUTM == 0 || OUTM == 1), "one wave's 64 columns, fp32 or 16-bit rows");
+  static_assert(PD >= 2 && PD <= RM, "residual ring depth");
+  constexpr bool BF16OUT = OUTM == 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int qr = lane >> 2, qc = lane & 3;  // read-back layout: row, first 16-B chunk
+  const int epi = EPI >= 0 ? EPI : a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
+  auto out_row = [&](int m) { return (epi & EPI_REMAP) ? remap_row(a, m) : m; };
+  const int ncol = nw + 4 * fq;
+  float4_t bias[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j)
+    bias[j] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)((lbias ? lbias : a.bias) + ncol + 16 * j)
+                                      : float4_t{0.f, 0.f, 0.f, 0.f};
+  const int fw = ((fr & 3) << 2) | (fr >> 2), fqr = ((qr & 3) << 2) | (qr >> 2);
+  const int gw = (((fr >> 1) & 1) << 2) | ((fr >> 2) & 3), gqr = (((qr >> 1) & 1) << 2) | ((qr >> 2) & 3);
+  // residual of group i (read-back layout: row mw + 16 i + qr, columns nw + 4 qc + 16 k)
+  float4_t res[PD][4];
+  auto load_res = [&](int i, float4_t (&dst)[4]) {
+    const float* src = a.res + (size_t)out_row(min(mw + 16 * i + qr, a.M - 1)) * a.ldr + nw + 4 * qc;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = *(const float4_t*)(src + 16 * k);
+  };
+  if (epi & AACLIP_EPI_RESID) {
+#pragma unroll
+    for (int i = 0; i < PD - 1; ++i) load_res(i, res[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    if ((epi & AACLIP_EPI_RESID) && i + PD - 1 < RM) load_res(i + PD - 1, res[(i + PD - 1) % PD]);
+    // bias + activation of all four column tiles first (independent chains: the VALU
+    // interleaves them; computing each tile at its LDS write measured 0.5 % slower)
+    float4_t v[RN];
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      v[j] = acc[i][j] + bias[j];
+      if (epi & AACLIP_EPI_GELU) {
+        const float2_t lo = gelu_fast2(float2_t{v[j][0], v[j][1]}), hi = gelu_fast2(float2_t{v[j][2], v[j][3]});
+        v[j] = float4_t{lo[0], lo[1], hi[0], hi[1]};
+      }
+      if (epi & AACLIP_EPI_QGELU) {
+        const float2_t lo = qgelu_fast2(float2_t{v[j][0], v[j][1]}), hi = qgelu_fast2(float2_t{v[j][2], v[j][3]});
+        v[j] = float4_t{lo[0], lo[1], hi[0], hi[1]};
+      }
+      if (epi & AACLIP_EPI_LEAKY)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[j][t] = v[j][t] >= 0.f ? v[j][t] : 0.01f * v[j][t];
+    }
+    const int m = mw + 16 * i + qr;
+    const size_t orow = (size_t)out_row(min(m, a.M - 1));
+    if (BF16OUT && !(epi & AACLIP_EPI_RESID)) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = 4 * q + 2 * (fq & 1) + (fq >> 1);
+        *(uint4*)(slot + (fr * 8 + (c ^ gw)) * 16) = pair_h16<H16>(v[2 * q], v[2 * q + 1], fq);
+      }
+      uint4 w[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) w[k] = *(const uint4*)(slot + (qr * 8 + ((qc + 4 * k) ^ gqr)) * 16);
+      if (a.dbg & 2) {  // diagnostic: everything but the global stores
+#pragma unroll
+        for (int k = 0; k < 2; ++k) asm volatile("" ::"v"(w[k].x), "v"(w[k].y), "v"(w[k].z), "v"(w[k].w));
+        continue;
+      }
+      if (m < a.M) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) *(uint4*)((uint16_t*)a.C + orow * a.ldc + nw + 8 * qc + 32 * k) = w[k];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RN; ++j) *(float4_t*)(slot + (fr * 16 + ((4 * j + fq) ^ fw)) * 16) = v[j];
+      float4_t u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        u[k] = *(const float4_t*)(slot + (qr * 16 + ((qc + 4 * k) ^ fqr)) * 16);
+        if (epi & AACLIP_EPI_RESID) u[k] += res[i % PD][k];
+      }
+      if (a.dbg & 2) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(u[k]));
+        continue;
+      }
+      if (m < a.M && BF16OUT) {  // 16-bit rows with a residual: 8 B per lane
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          *(uint2*)((uint16_t*)a.C + orow * a.ldc + nw + 4 * qc + 16 * k) =
+              uint2{pack_h16x2<H16>(u[k][0], u[k][1]), pack_h16x2<H16>(u[k][2], u[k][3])};
+      } else if (m < a.M) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) *(float4_t*)((float*)a.C + orow * a.ldc + nw + 4 * qc + 16 * k) = u[k];
+        if (epi & AACLIP_EPI_AUX_BF16) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            *(uint2*)((uint16_t*)a.aux + orow * a.ldaux + nw + 4 * qc + 16 * k) =
+                uint2{pack_h16x2<H16>(u[k][0], u[k][1]), pack_h16x2<H16>(u[k][2], u[k][3])};
+        }
       }
     }
   }
@@ -827,9 +946,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
     // both wave rows run the epilogue together (row 0 waits out row 1's last phase);
     // row 1 re-takes its one-barrier lag before the next tile
     if (wr == 0) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // the epilogue's LDS slot writes stay behind that barrier
     const int mw = m0 + wr * TM, nw = n0 + wc * TN;
     const float* lbp = (const float*)(smem + 2 * STAGE) - n0;  // staged bias, by column
-    const float* lb = lds_bias ? lbp : nullptr;
+    // the epilogue's per-wave 4-KiB LDS slot: regions A1 / B1 of the last K-step's stage,
+    // whose last reads (P3 / P2) every wave finished before the barrier above and which
+    // no phantom DMA targets (those fill the other stage and this stage's A0 / B0)
+    char* slot = smem + ((nk - 1) & 1) * STAGE + (wr ? 3 : 1) * REGION + wc * 4096;
     // S for the next tile's first K-step: a LOWER bound on the VMEM ops this epilogue
     // issues between the next tile's prefetched regions and its own next DMA (stores;
     // the bias / residual loads only add to it). Edge tiles skip whole row groups: 0.
@@ -847,11 +970,14 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       else
         wave_epilogue<RM, RN, 3, 0, 0, H16>(a, acc, mw, nw, lane);
     } else {
-#define EPI_CASE(BF, E, NS)                                               \
-  if (bf16_out == (BF) && key == (E)) {                                   \
-    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane,    \
-                                                 (!PERSIST && ((E) & AACLIP_EPI_BIAS)) ? lbp : nullptr); \
-    s_prev = full && !(a.dbg & 2) ? (NS) : 0;                             \
+#define EPI_CASE(BF, E, NS)                                                                      \
+  if (bf16_out == (BF) && key == (E)) {                                                          \
+    if constexpr (PERSIST)                                                                       \
+      wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane);                        \
+    else                                                                                         \
+      wave_epilogue_lds<RM, RN, BF ? 1 : 0, E, H16>(a, acc, mw, nw, lane,                        \
+                                                    ((E) & AACLIP_EPI_BIAS) ? lbp : nullptr, slot); \
+    s_prev = full && !(a.dbg & 2) ? (NS) : 0;                                                    \
   } else
       EPI_CASE(true, AACLIP_EPI_BIAS, RM * RN / 2)
       EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU, RM * RN / 2)
@@ -860,10 +986,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16, RM * RN + RM * RN / 2)
       EPI_CASE(false, AACLIP_EPI_LEAKY, RM * RN)
 #undef EPI_CASE
-      if (bf16_out)
-        wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane, lb);
-      else
-        wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane, lb);
+      // any other flag combination (row remap, 16-bit rows + residual, ...): run-time flags
+      if constexpr (PERSIST) {
+        if (bf16_out)
+          wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane);
+        else
+          wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane);
+      } else {
+        if (bf16_out)
+          wave_epilogue_lds<RM, RN, 1, -1, H16>(a, acc, mw, nw, lane, lds_bias ? lbp : nullptr, slot);
+        else
+          wave_epilogue_lds<RM, RN, 0, -1, H16>(a, acc, mw, nw, lane, lds_bias ? lbp : nullptr, slot);
+      }
     }
     if (!PERSIST || !has_next) break;
     if (wr == 1) __builtin_amdgcn_s_barrier();

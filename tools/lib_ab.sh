@@ -1,10 +1,10 @@
 # A/B of two builds of libaaclip_hip.so (AACLIP_LIB) on one box, interleaved rounds:
 # the whole C2 step (bench.py, hipGraph) and, with ATTN=1, the attention kernel alone.
-# usage (GPU box): bash tools/lib_ab.sh ab/libaaclip_base.so aa-clip_amd/aaclip/libaaclip_hip.so
+# usage (GPU box): [ROUNDS=3] bash tools/lib_ab.sh ab/libaaclip_base.so aa-clip_amd/aaclip/libaaclip_hip.so
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-for r in 1 2 3; do
+for r in $(seq ${ROUNDS:-3}); do
   for lib in "$@"; do
     if [ "${ATTN:-0}" = 1 ]; then
       AACLIP_LIB=$lib timeout -k 10 120 python tools/attn_variants.py --variants 3 --seqs 577,1025 \
