@@ -383,10 +383,13 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
 // fp32 rows: 16 chunks of 16 B, chunk c of row r at c ^ f(r), f(r) = (r & 3) << 2 | r >> 2;
 // 16-bit rows: 8 chunks, slot 8r + (c ^ g(r)), g(r) = ((r >> 1) & 1) << 2 | (r >> 2) & 3
 // (16-bit rows with a residual take the fp32 form and store 8 B per lane).
-template <int RM, int RN, int OUTM, int EPI, bool H16, int PD = 2>
+// fp8 MX rows (OUTM 2, the fp8 kernel's c_fc): the 64-B row of e4m3 bytes after
+// transpose_fq, 4 chunks, slot 4r + (c ^ (r >> 2)); SCALED 2 as in wave_epilogue.
+template <int RM, int RN, int OUTM, int EPI, bool H16, int SCALED = 0, int PD = 2>
 __device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
                                                   int lane, const float* lbias, char* slot) {
-  static_assert(RN == 4 && (OUTM == 0 || OUTM == 1), "one wave's 64 columns, fp32 or 16-bit rows");
+  static_assert(RN == 4 && OUTM >= 0 && OUTM <= 2, "one wave's 64 columns: fp32, 16-bit or fp8 MX rows");
+  static_assert(SCALED == 0 || SCALED == 2, "no per-row A scales");
   static_assert(PD >= 2 && PD <= RM, "residual ring depth");
   constexpr bool BF16OUT = OUTM == 1;
   const int fr = lane & 15, fq = lane >> 4;
@@ -399,6 +402,11 @@ __device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&
   for (int j = 0; j < RN; ++j)
     bias[j] = (epi & AACLIP_EPI_BIAS) ? *(const float4_t*)((lbias ? lbias : a.bias) + ncol + 16 * j)
                                       : float4_t{0.f, 0.f, 0.f, 0.f};
+  float4_t wsc[RN];  // fp8: per-column weight scales of this lane's 4 columns in tile j
+  if constexpr (SCALED) {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) wsc[j] = *(const float4_t*)(a.w_scale + ncol + 16 * j);
+  }
   const int fw = ((fr & 3) << 2) | (fr >> 2), fqr = ((qr & 3) << 2) | (qr >> 2);
   const int gw = (((fr >> 1) & 1) << 2) | ((fr >> 2) & 3), gqr = (((qr >> 1) & 1) << 2) | ((qr >> 2) & 3);
   // residual of group i (read-back layout: row mw + 16 i + qr, columns nw + 4 qc + 16 k)
@@ -420,7 +428,10 @@ __device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&
     float4_t v[RN];
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
-      v[j] = acc[i][j] + bias[j];
+      if constexpr (SCALED == 2)
+        v[j] = acc[i][j] * wsc[j] + bias[j];
+      else
+        v[j] = acc[i][j] + bias[j];
       if (epi & AACLIP_EPI_GELU) {
         const float2_t lo = gelu_fast2(float2_t{v[j][0], v[j][1]}), hi = gelu_fast2(float2_t{v[j][2], v[j][3]});
         v[j] = float4_t{lo[0], lo[1], hi[0], hi[1]};
@@ -435,6 +446,35 @@ __device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&
     }
     const int m = mw + 16 * i + qr;
     const size_t orow = (size_t)out_row(min(m, a.M - 1));
+    if constexpr (OUTM == 2) {
+      float amax = 0.f;
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) amax = fmaxf(amax, fabsf(v[j][t]));
+      const int e = mx_exp(max_over_fq(amax));
+      const float inv = pow2i(-e);
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(v[j][0] * inv, v[j][1] * inv, 0, false);
+        d[j] = __builtin_amdgcn_cvt_pk_fp8_f32(v[j][2] * inv, v[j][3] * inv, w, true);
+      }
+      transpose_fq(d);  // lane (fr, fq): row fr, bytes 16 fq .. 16 fq + 15
+      *(uint4*)(slot + (4 * fr + (fq ^ (fr >> 2))) * 16) = uint4{d[0], d[1], d[2], d[3]};
+      const uint4 w = *(const uint4*)(slot + (4 * qr + (qc ^ (qr >> 2))) * 16);
+      if (a.dbg & 2) {
+        asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
+        continue;
+      }
+      if (m < a.M) *(uint4*)((uint8_t*)a.C + orow * a.ldc + nw + 16 * qc) = w;
+      const int mr = mw + 16 * i + fr;  // the block scale: one byte per row, lanes fq = 0
+      if (mr < a.M && fq == 0) {
+        const int blk = nw >> 6;
+        a.c_mx[((size_t)(blk >> 1) * a.ld_cmx + out_row(mr)) * 2 + (blk & 1)] = (uint8_t)(e + 127);
+      }
+      continue;
+    }
     if (BF16OUT && !(epi & AACLIP_EPI_RESID)) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -1166,13 +1206,17 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
       for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
+  asm volatile("" ::: "memory");  // the epilogue's LDS slot writes stay behind that barrier
   const int mw = m0 + wr * TM, nw = n0 + wc * TN;
   const int key = a.epi;
   const int outm = a.out_dtype == AACLIP_F32 ? 0 : (a.out_dtype == AACLIP_BF16 ? 1 : 2);
-#define EPI_CASE(OM, E)                                                \
-  if (outm == (OM) && key == (E)) {                                    \
-    wave_epilogue<RM, RN, OM, E, 2>(a, acc, mw, nw, lane);             \
-    return;                                                            \
+  // quad-coalesced epilogue through the same per-wave LDS slot as the bf16 8-phase
+  // kernel (A1 / B1 of the last K-step's stage: no phantom DMA lands there)
+  char* eslot = smem + ((nk - 1) & 1) * STAGE + (wr ? 3 : 1) * REGION + wc * 4096;
+#define EPI_CASE(OM, E)                                                         \
+  if (outm == (OM) && key == (E)) {                                             \
+    wave_epilogue_lds<RM, RN, OM, E, false, 2>(a, acc, mw, nw, lane, nullptr, eslot); \
+    return;                                                                     \
   }
   EPI_CASE(1, AACLIP_EPI_BIAS)                                          // qkv
   EPI_CASE(0, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)                       // out-proj, c_proj
