@@ -51,7 +51,6 @@ SIGNATURES = {
     "aaclip_gemm_scores": [_I, _I, _I, _I, _P, _L, _P, _L, _I, _P, _I, _P, _L, _P],
     "aaclip_anomaly_map_partials": [_P, _L, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P],
     "aaclip_layernorm": [_I, _P, _L, _P, _P, _P, _L, _I, _I, _P, _L, _P],
-    "aaclip_residual_layernorm": [_I, _P, _P, _P, _P, _P, _I, _I, _P, _L, _P],
     "aaclip_text_embed_ln": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "aaclip_eot_ln": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "aaclip_anchor_reduce": [_P, _I, _I, _P, _I, _I, _P],
@@ -61,8 +60,6 @@ SIGNATURES = {
     "aaclip_blur_upsample": [_P, _P, _I, _I, _I, _I, _I, _F, _I, _P],
     "aaclip_anomaly_map": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P],
     "aaclip_image_score": [_I, _P, _L, _P, _I, _I, _I, _I, _P, _P, _P, _P],
-    "aaclip_anomaly_map_score": [_I, _P, _I, _L, _P, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P],
-    "aaclip_anomaly_map_fused": [_I, _P, _I, _L, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P],
     "aaclip_metrics_workspace": [_L, _I, ctypes.POINTER(ctypes.c_size_t)],
     "aaclip_metrics_eval": [_P, _P, _P, _P, _I, _L, _I, _P, ctypes.c_size_t, _P, _P],
     "aaclip_bicubic_taps": [_I, _I, ctypes.POINTER(_I)],

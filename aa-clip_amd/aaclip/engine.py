@@ -162,21 +162,12 @@ class VisualEngine:
         self.relu = r_det
         self.w_seg = [cdt(t) for t in self.w_seg[:-1]] + [cdt(torch.cat([self.w_seg[-1], w_det], 0))]
         self._ws = {}
-        # the one-launch map (aaclip_anomaly_map_fused) is bit-identical but measured 115-119 us
-        # in-step vs 61 us for the two launches (agent-scope release/acquire per workgroup,
-        # 3 patch rows per wave: profiles/r03/map_fused_ab.txt): opt-in, AACLIP_MAP_FUSED=1
-        self.map_fused = os.environ.get("AACLIP_MAP_FUSED", "0") == "1"
         self.poison = False  # tests: fill new workspaces with NaN (read-before-write screen)
-        # deferred out-proj residual (A/B, AACLIP_DEFER_RESID=1): out-proj writes acc + bias to
-        # the u workspace with no residual read, and ln_2 does x += d before normalising
-        # (aaclip_residual_layernorm; the same fp32 add, bit-identical)
-        self.defer_resid = os.environ.get("AACLIP_DEFER_RESID", "0") == "1"
         # predict(): projections straight into map partials (aaclip_gemm_scores +
         # aaclip_anomaly_map_partials) instead of segbuf rows + a stream over them;
-        # AACLIP_MAP_PARTIALS=0 restores the row path (A/B)
+        # AACLIP_MAP_PARTIALS=0 restores the row path (A/B). Captured graphs are keyed on it
+        # (predict_cached).
         self.map_partials = os.environ.get("AACLIP_MAP_PARTIALS", "1") == "1"
-        self.stream_prio = 0  # A/B: 1 = the first chunk stream at high priority (_chunk_streams)
-        self.stagger = 0  # A/B: chunk 1 waits for chunk 0's first `stagger` block sub-ops (predict)
 
     # ------------------------------------------------------------------ workspace
     def _workspace(self, B: int, S: int, slot: int = 0):
@@ -246,7 +237,6 @@ class VisualEngine:
                         t.fill_(float("nan"))
                     else:
                         t.view(torch.uint8).fill_(0xFF)
-        ws["bandcnt"] = ops.map_band_counters(B, S, dev)  # zero; every fused map launch leaves it zero
         if TUNE and cdt != torch.float32:
             self._tune(ws)
         return ws
@@ -272,13 +262,11 @@ class VisualEngine:
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
     @_on_device
-    def forward_raw(self, x: torch.Tensor, slot: int = 0, T: torch.Tensor | None = None, mark=None):
+    def forward_raw(self, x: torch.Tensor, slot: int = 0, T: torch.Tensor | None = None):
         """Run the visual tower; returns (seg_raw list of [B*P, 768] views,
         det_raw [B*P, 768] view, workspace). Rows are unnormalised projections.
         With T (predict, 16-bit modes) the projections are written as anomaly-map
-        partials against T into ws["spart"] instead, and (None, None, ws) is returned.
-        mark = (k, event): record `event` on the current stream after block sub-op k
-        (4 per block: qkv, attention, out-proj, MLP) -- the chunk stagger of predict()."""
+        partials against T into ws["spart"] instead, and (None, None, ws) is returned."""
         if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != x.shape[3] or x.shape[2] % PATCH:
             raise ValueError("input must be [B, 3, S, S] with S a multiple of 14")
         x = x.to(self.device, torch.float32).contiguous()
@@ -320,19 +308,11 @@ class VisualEngine:
             def attend():
                 ops.attention(ws["qkv"], ws["attn"], B, n_tok, HEADS, q_prescaled=self.q_prescaled)
 
-            defer = self.defer_resid
-
             def out_proj(blk):
-                if defer:  # acc + bias only; ln_2 adds it to x (ln2 below)
-                    ops.gemm(ws["attn"], blk["w_o"], ws["u"], bias=blk["b_o"])
-                else:
-                    ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
+                ops.gemm(ws["attn"], blk["w_o"], X, bias=blk["b_o"], residual=X)
 
             def ln2(blk, y, y_sc=None):
-                if defer:
-                    ops.residual_layernorm(X, ws["u"], blk["ln2"][0], blk["ln2"][1], y, y_sc=y_sc)
-                else:
-                    ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], y, y_sc=y_sc)
+                ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], y, y_sc=y_sc)
 
             def mlp(blk, aux):
                 if self.fp8_mlp_only:  # ln_2 -> MX e4m3 -> c_fc (fp8, GELU, MX out) -> c_proj (fp8)
@@ -346,21 +326,13 @@ class VisualEngine:
                 ln2(blk, H)
                 ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=self.act)
                 ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=aux)
-        def tick(k):
-            if mark is not None and mark[0] == k:
-                mark[1].record(torch.cuda.current_stream(self.device))
-
         for i in range(last):
             blk = self.blocks[i]
             qkv(blk)
-            tick(4 * i)
             attend()
-            tick(4 * i + 1)
             out_proj(blk)
-            tick(4 * i + 2)
             adapt = i < self.adapt_until
             mlp(blk, ws["xb"] if (adapt and ws["xb"] is not None) else None)
-            tick(4 * i + 3)
             tap = ws["taps"][lvl[i + 1]] if (i + 1) in lvl else None
             nxt = self.blocks[i + 1]["ln1"] if i + 1 < last else None
             u = None
@@ -417,33 +389,20 @@ class VisualEngine:
         return [y.view(B, P, EMBED) for y in out], det
 
     def _tail(self, seg_raw, det_raw, ws, T, out_map, out_score, k, s):
-        """Anomaly map + image score of one chunk from its projections. Two passes over
-        segbuf (the level features, then the det rows): measured 4 % faster than the one
-        pass of aaclip_anomaly_map_score (62.7 vs 65.1 us at B = 32, tools/map_ab.py), whose
-        16-row workgroups stream at 4.6 TB/s where the one-row-per-wave map pass reaches
-        6.4; the one-pass entry stays in the ABI, bit-identical (tests). The map itself is
-        two launches (patch scores, then blur + upsample); AACLIP_MAP_FUSED=1 selects the
-        one-launch aaclip_anomaly_map_fused (same bits, measured 2x slower in the step)."""
+        """Anomaly map + image score of one chunk from its projections: from the GEMM-emitted
+        partials (predict, 16-bit modes), else two passes over segbuf (the level features,
+        then the det rows). One-pass and one-launch forms measured slower (round 3) and were
+        removed in round 5."""
         if seg_raw is None:  # projections as partials (forward_raw with T)
             ops.anomaly_map_partials(ws["spart"], len(self.levels), out_map, ws["grid"], g=ws["g"], ksize=k, sigma=s,
                                      det_ws=ws["detrow"], score=out_score)
             return
-        if self.map_fused:
-            ops.anomaly_map_fused(seg_raw, T, out_map, ws["grid"], ws["bandcnt"], g=ws["g"], ksize=k, sigma=s)
-        else:
-            ops.anomaly_map(seg_raw, T, out_map, ws["grid"], g=ws["g"], ksize=k, sigma=s)
+        ops.anomaly_map(seg_raw, T, out_map, ws["grid"], g=ws["g"], ksize=k, sigma=s)
         ops.image_score(det_raw, out_map.shape[0], ws["P"], ws["partial"], det=ws["det"], T=T, score=out_score)
 
     def _chunk_streams(self, n: int):
-        # stream_prio (A/B): the first chunk's stream at high priority, so the dispatcher
-        # serves its workgroups first and the chunks drift apart (one chunk's tile-starved
-        # launches then share the CUs with the other's row kernels and wide GEMMs)
-        prio = int(getattr(self, "stream_prio", 0))
-        key = (n, prio)
-        if getattr(self, "_streams_key", None) != key:
-            self._streams = [torch.cuda.Stream(device=self.device, priority=(-1 if (prio and i == 0) else 0))
-                             for i in range(n)]
-            self._streams_key = key
+        if len(getattr(self, "_streams", [])) < n:
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(n)]
         return self._streams[:n]
 
     @torch.no_grad()
@@ -513,19 +472,16 @@ class VisualEngine:
         # images per chunk): whole two-stream C2 step 2240 -> 2295 images/s bf16 (2164 ->
         # 2220 fp16); a single stream keeps the heuristic (1895 vs 2050). Thread-local
         # (aaclip_gemm_concurrent), chosen at launch, so graph capture keeps it.
-        # stagger (A/B): chunk 1 starts after chunk 0 has enqueued `stagger` block sub-ops
-        stag = int(getattr(self, "stagger", 0)) if nstreams > 1 else 0
-        sev = torch.cuda.Event() if stag else None
+        # (holding chunk 1 back by a few block sub-ops, or its stream at a lower priority,
+        # measured 0.3-3.5 % slower: the free-running chunks drift into a good pairing,
+        # profiles/r04/chunk_stagger_ab.txt, stream_priority_ab.txt)
         with ops.concurrent_gemms(nstreams > 1 and self.dtype in (torch.bfloat16, torch.float16)):
             for i in range(len(sizes)):
                 b0, b1 = bounds[i], bounds[i + 1]
                 st = sts[i % nstreams]
-                if stag and i == 1:
-                    st.wait_event(sev)
                 with torch.cuda.stream(st):
                     seg_raw, det_raw, ws = self.forward_raw(x[b0:b1], slot=_slot0 + i % nstreams,
-                                                            T=T if self.map_partials else None,
-                                                            mark=(stag, sev) if (stag and i == 0) else None)
+                                                            T=T if self.map_partials else None)
                     self._tail(seg_raw, det_raw, ws, T, out_map[b0:b1], out_score[b0:b1], k, s)
         for st, ev in zip(sts, done):
             ev.record(st)
@@ -544,7 +500,9 @@ class VisualEngine:
         not coming back) and never evicts a full-batch graph; eviction is least recently
         used. Same kernels, same bits (tests/test_e2e_gpu.py); the outputs are
         graph-owned buffers, overwritten by the next replay of that shape."""
-        key = (x.shape[0], x.shape[-1], domain, tuple(streams) if isinstance(streams, (tuple, list)) else streams)
+        # every engine setting that changes what a capture records is part of the key
+        key = (x.shape[0], x.shape[-1], domain, tuple(streams) if isinstance(streams, (tuple, list)) else streams,
+               bool(self.map_partials))
         if not hasattr(self, "_graph_cache"):
             self._graph_cache, self._last_key = {}, None
         run = self._graph_cache.get(key)

@@ -417,23 +417,6 @@ def layernorm(x, w, b, y, y_sc=None):
     return y
 
 
-def residual_layernorm(x, d, w, b, y, y_sc=None):
-    """x += d (in place, fp32: the deferred out-proj residual add), then y = LN(x)
-    (aaclip_residual_layernorm). Bit-identical to gemm(..., residual=x) + layernorm."""
-    _dev(x, d, y)
-    for t, n in ((x, "x"), (d, "d"), (y, "y")):
-        _rowmajor(t, n)
-    if x.shape != y.shape or x.shape != d.shape or x.dtype != torch.float32 or d.dtype != torch.float32:
-        raise ValueError("residual_layernorm shape/dtype mismatch")
-    if not (x.is_contiguous() and d.is_contiguous() and (y.is_contiguous() or y_sc is not None)):
-        raise ValueError("residual_layernorm needs contiguous rows")
-    od, scp, ld = _mx_out(y, y_sc, x.shape[0])
-    _launch("residual_layernorm", "residual_ln_kernel", 0.0, x.numel() * 12 + y.numel() * y.element_size(),
-            "aaclip_residual_layernorm", od, _ptr(x), _ptr(d), _ptr(w), _ptr(b), _ptr(y), x.shape[0], x.shape[1],
-            scp, ld, _stream())
-    return y
-
-
 def text_embed_ln(tokens, tok_emb, pos, ln1, x, h):
     _dev(tokens, x, h)
     n, ctx = tokens.shape
@@ -589,33 +572,6 @@ def anomaly_map_partials(part, n_levels, out, grid_ws, *, g, ksize, sigma, det_w
     return out
 
 
-def map_band_counters(B: int, S: int, device) -> torch.Tensor:
-    """Zeroed band counters for anomaly_map_fused (B * ceil(S / 8) int32); every fused call
-    leaves them zero again. One set per concurrently running call (per chunk workspace)."""
-    return torch.zeros(B * ((S + 7) // 8), device=device, dtype=torch.int32)
-
-
-def anomaly_map_fused(levels, T, out, grid_ws, counters, *, g, ksize, sigma):
-    """anomaly_map in one launch (aaclip_anomaly_map_fused): same bits; counters from
-    map_band_counters(B, S)."""
-    _dev(*levels, T, out, grid_ws, counters)
-    B, S, S2 = out.shape
-    rows, C = levels[0].shape
-    if rows != B * g * g or S != S2 or grid_ws.numel() < rows or grid_ws.dtype != torch.float32:
-        raise ValueError("anomaly_map_fused shape mismatch (grid_ws: fp32 >= [B*g*g])")
-    if counters.dtype != torch.int32 or counters.numel() < B * ((S + 7) // 8) or not out.is_contiguous():
-        raise ValueError("anomaly_map_fused: counters int32 >= B*ceil(S/8), contiguous output")
-    for t in levels:
-        if t.shape != (rows, C) or t.stride(0) != levels[0].stride(0) or t.dtype != levels[0].dtype:
-            raise ValueError("levels must share shape, dtype and stride")
-    arr = _level_array(levels)
-    nb = len(levels) * rows * C * levels[0].element_size() + C * 2 * 4 + B * S * S * 4 + 2 * rows * 4
-    _launch("anomaly_map", "anomaly_map (map_fused_kernel)", 0.0, nb, "aaclip_anomaly_map_fused",
-            dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(T), B, g, C, S, ksize, float(sigma),
-            _ptr(grid_ws), _ptr(counters), _ptr(out), _stream())
-    return out
-
-
 def image_score(det_raw, batch, n_patch, partial, det=None, T=None, score=None, normalize=True):
     _dev(det_raw, partial, det, T, score)
     _rowmajor(det_raw, "det_raw")
@@ -625,31 +581,6 @@ def image_score(det_raw, batch, n_patch, partial, det=None, T=None, score=None, 
     _launch("image_score", "image_score (det_partial + det_finalize)", 0.0, rows * C * det_raw.element_size(),
             "aaclip_image_score", dtag(det_raw), _ptr(det_raw), det_raw.stride(0), _ptr(T), batch, n_patch, C,
             int(normalize), _ptr(partial), _ptr(det), _ptr(score), _stream())
-
-
-def anomaly_map_score(levels, det_raw, T, out, grid_ws, partial, score, *, g, ksize, sigma, det=None):
-    """The test path's per-batch tail in one pass over the projections (aaclip_anomaly_map_score):
-    the level-summed map of the normalised levels [B*g*g, 768] each, blur + upsample into
-    out [B, S, S], and the image score from det_raw (same row stride as the levels)."""
-    _dev(*levels, det_raw, T, out, grid_ws, partial, score, det)
-    B, S, S2 = out.shape
-    rows, C = levels[0].shape
-    if rows != B * g * g or S != S2 or grid_ws.numel() < rows or grid_ws.dtype != torch.float32:
-        raise ValueError("anomaly_map_score shape mismatch (grid_ws: fp32 >= [B*g*g])")
-    if not out.is_contiguous() or score.numel() < B or partial.numel() < B * ((g * g + 15) // 16) * C:
-        raise ValueError("anomaly_map_score output / workspace too small")
-    for t in list(levels) + [det_raw]:
-        if t.shape != (rows, C) or t.stride(0) != levels[0].stride(0) or t.dtype != levels[0].dtype:
-            raise ValueError("levels and det_raw must share shape, dtype and stride")
-    if det is not None and det.shape != (B, C):
-        raise ValueError("det must be [B, 768]")
-    arr = _level_array(levels)
-    nb = (len(levels) + 1) * rows * C * levels[0].element_size() + C * 2 * 4 + B * S * S * 4 + 2 * rows * 4
-    _launch("anomaly_map", "anomaly_map_score (map_det + blur_upsample + det_finalize)", 0.0, nb,
-            "aaclip_anomaly_map_score", dtag(levels[0]), arr, len(levels), levels[0].stride(0), _ptr(det_raw),
-            _ptr(T), B, g, C, S, ksize, float(sigma), _ptr(grid_ws), _ptr(partial), _ptr(out), _ptr(det),
-            _ptr(score), _stream())
-    return out, score
 
 
 def metrics_eval(pixel_preds: torch.Tensor, pixel_label: torch.Tensor, image_preds: torch.Tensor,

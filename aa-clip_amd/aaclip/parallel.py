@@ -96,10 +96,13 @@ def gather_rows_to(local: torch.Tensor, n_total: int, dst: int = 0, group=None):
     rank = dist.get_rank(group)
     sizes = [shard_range(n_total, r, world) for r in range(world)]
     width = max(b - a for a, b in sizes)
-    pad = torch.zeros((width,) + tuple(local.shape[1:]), device=local.device, dtype=local.dtype)
+    # gloo's gather takes host tensors only (the one-GPU rehearsal of the multi-rank harness:
+    # every rank on cuda:0 over gloo); RCCL gathers device memory directly
+    host = str(dist.get_backend(group)) == "gloo"
+    pad = torch.zeros((width,) + tuple(local.shape[1:]), device="cpu" if host else local.device, dtype=local.dtype)
     pad[: local.shape[0]] = local
     bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
     dist.gather(pad, gather_list=bufs, dst=dst, group=group)
     if rank != dst:
         return None
-    return torch.cat([bufs[r][: b - a] for r, (a, b) in enumerate(sizes)], 0)
+    return torch.cat([bufs[r][: b - a] for r, (a, b) in enumerate(sizes)], 0).to(local.device)

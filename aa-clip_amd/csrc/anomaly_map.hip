@@ -173,8 +173,8 @@ constexpr int kMaxC = 8;  // channels of the train branch (anchors), softmax ove
 // lambdas: no FMA contraction). K = ksize at compile time for the domains' 7 and 9
 // (tap loads issued together), -1 = any ksize at run time, 0 = no blur.
 // LDS: C * (2 * xrows + brows) * g floats, sized by the host for the band.
-// The band body is a device function: blur_upsample_kernel runs it for one (image, band)
-// per workgroup, map_fused_kernel for the bands its workgroup completes (same bits).
+// The band body is a device function: blur_upsample_kernel and blur_upsample_score_kernel
+// run it for one (image, band) per workgroup.
 template <int C, int K>
 __device__ __forceinline__ void blur_band(const float* grid, float* out, int b, int band, int g, int S,
                                           int ksize_rt, const Gauss& gw, int softmax, float scale, int xrows,
@@ -403,112 +403,22 @@ __global__ __launch_bounds__(64) void blur_upsample_score_kernel(const float* gr
   blur_band<1, K>(grid, out, blockIdx.y, blockIdx.x, g, S, ksize_rt, gw, 0, scale, xrows, brows, smem, threadIdx.x);
 }
 
-// Source grid rows [x_lo, x_hi] one output band reads (blur_band: the bilinear taps'
-// rows r_lo..r_hi and their blur neighbourhood, clamped; reflected indices stay inside).
-__device__ __forceinline__ void band_rows(int band, int g, int S, int ksize, float scale, int& x_lo, int& x_hi) {
-  const int y0 = band * kBand;
-  const int y1 = min(y0 + kBand, S);
-  const int r_lo = (int)(scale * (float)y0);
-  const int r_hi = min((int)(scale * (float)(y1 - 1)) + 1, g - 1);
-  const int r = ksize / 2;
-  x_lo = ksize > 0 ? max(0, r_lo - r) : r_lo;
-  x_hi = ksize > 0 ? min(g - 1, r_hi + r) : r_hi;
-}
-
-// The whole test-branch map in ONE launch: workgroup (r, b) streams the g patch rows of
-// grid row r of image b through every level (patch_row_score, the bits of
-// patch_scores_kernel; 8 waves, each wave one patch position at a time), writes the
-// level-summed scores to grid, and then counts itself into every output band whose
-// source rows [x_lo, x_hi] hold row r (one device-scope atomic per band). The workgroup
-// whose count completes a band computes that band (blur_band, the bits of
-// blur_upsample_kernel) and zeroes its counter for the next launch: no workgroup ever
-// waits for another, and the blur + upsample runs in the tail of the stream instead of
-// a second launch. Ordering: each wave's grid stores complete (vmcnt) before the
-// barrier, wave 0 releases at agent scope before its atomics, a band's computing wave
-// acquires at agent scope before it reads the grid (the grid rows come from other
-// workgroups, other XCDs' L2s). cnt: batch * nbands int32, zero before the first launch.
-constexpr int kFusedWaves = 8;
-constexpr int kMaxBands = 128;  // out_size <= 1024
-
-template <bool F32IN, int NLMAX, int K>
-__global__ __launch_bounds__(64 * kFusedWaves, NLMAX <= 4 ? 4 : 2) void map_fused_kernel(LevelPtrs lv, int nl, int64_t ld,
-                                                                    const float* T, int g, int S, int ksize_rt,
-                                                                    Gauss gw, float scale, int xrows, int brows,
-                                                                    int nbands, float* grid, int* cnt, float* out) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];  // kFusedWaves band-staging slices
-  __shared__ int ready[kMaxBands];
-  __shared__ int nready;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int r = blockIdx.x, b = blockIdx.y;
-  const int ksize = K >= 0 ? K : ksize_rt;
-  {
-    float4_t t0[3], t1[3];
-    load_anchors(T, t0, t1, lane);
-    for (int j = wid; j < g; j += kFusedWaves) {
-      const size_t row = ((size_t)b * g + r) * g + j;
-      const float acc = patch_row_score<F32IN, NLMAX>(lv, nl, ld, row, t0, t1, 1, 0, 1, nullptr, lane);
-      if (lane == 0) grid[row] = acc;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's grid stores are in L2
-  __syncthreads();
-  if (wid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    int n = 0;
-    for (int k0 = 0; k0 < nbands; k0 += 64) {
-      const int k = k0 + lane;
-      bool done = false;
-      if (k < nbands) {
-        int x_lo, x_hi;
-        band_rows(k, g, S, ksize, scale, x_lo, x_hi);
-        if (x_lo <= r && r <= x_hi) {
-          int* c = cnt + (size_t)b * nbands + k;
-          const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          done = old + 1 == x_hi - x_lo + 1;
-          if (done) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      const uint64_t m = __builtin_amdgcn_ballot_w64(done);
-      if (done) ready[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = k;
-      n += __builtin_popcountll(m);
-    }
-    if (lane == 0) nready = n;
-  }
-  __syncthreads();
-  const int n = nready;
-  if (wid < n) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    float* slice = smem + (size_t)wid * (2 * xrows + brows) * g;
-    for (int i = wid; i < n; i += kFusedWaves)
-      blur_band<1, K>(grid, out, b, ready[i], g, S, ksize_rt, gw, 0, scale, xrows, brows, slice, lane);
-  }
-}
-
-// Image score, stage 1 -- fused with stage 1 of the anomaly map (NL > 0 levels): one
-// workgroup per (image, chunk of kDetRows = 16 patch rows). W = 16 waves take one row
-// each (W = 4: four rows each, in sequence, for NL = 7, 8, whose levels would not fit
-// the 128 registers a 16-wave workgroup allows). Per row the wave reads the det_proj row
-// (segbuf's last 768 columns: the levels' row stride), normalises it into its LDS slot
-// and, with levels, reads that row in every level and writes the level-summed score
-// (patch_row_score: the same bits as patch_scores_kernel) -- one pass over segbuf
-// instead of two. The 16 slots meet in a fixed tree per column, whatever W or NL:
-// partial[b][chunk][j] = ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)) + (same for s8..s15),
-// so the fused pass and aaclip_image_score (NL = 0) give the same det bits.
+// Image score, stage 1: one workgroup per (image, chunk of kDetRows = 16 patch rows),
+// 16 waves, one row each. Per row the wave reads the det_proj row, normalises it into
+// its LDS slot; the 16 slots meet in a fixed tree per column,
+// partial[b][chunk][j] = ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)) + (same for s8..s15).
+// (A one-pass form that also scored the level rows -- aaclip_anomaly_map_score --
+// measured slower than two passes and was removed in round 5.)
 constexpr int kDetRows = 16;
 
-template <int NL, bool F32IN, int W>
-__global__ __launch_bounds__(64 * W) void map_det_kernel(LevelPtrs lv, int64_t ld, const void* det, const float* T,
-                                                         int n_patch, int normalize, float* grid, float* partial,
-                                                         int nchunk) {
-  static_assert(kDetRows % W == 0, "rows per wave");
+template <bool F32IN>
+__global__ __launch_bounds__(64 * kDetRows) void map_det_kernel(int64_t ld, const void* det, int n_patch,
+                                                                int normalize, float* partial, int nchunk) {
   __shared__ float red[kDetRows][768];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int b = blockIdx.y, ch = blockIdx.x;
-  float4_t t0[3], t1[3];
-  if constexpr (NL > 0) load_anchors(T, t0, t1, lane);
-#pragma unroll 1
-  for (int k = 0; k < kDetRows / W; ++k) {
-    const int slot = wid * (kDetRows / W) + k;
+  {
+    const int slot = wid;
     const int p = ch * kDetRows + slot;
     float4_t v[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
     if (p < n_patch) {
@@ -526,10 +436,6 @@ __global__ __launch_bounds__(64 * W) void map_det_kernel(LevelPtrs lv, int64_t l
                           __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u)};
         }
       }
-      if constexpr (NL > 0) {
-        const float score = patch_row_score<F32IN, NL>(lv, NL, ld, row, t0, t1, normalize, 0, 1, nullptr, lane);
-        if (lane == 0) grid[row] = score;
-      }
       float ss = 0.f;
 #pragma unroll
       for (int c = 0; c < 3; ++c)
@@ -544,7 +450,7 @@ __global__ __launch_bounds__(64 * W) void map_det_kernel(LevelPtrs lv, int64_t l
     for (int c = 0; c < 3; ++c) *(float4_t*)&red[slot][256 * c + 4 * lane] = v[c];
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < 768; j += 64 * W) {
+  for (int j = threadIdx.x; j < 768; j += 64 * kDetRows) {
     float h[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) h[i] = red[2 * i][j] + red[2 * i + 1][j];
@@ -757,52 +663,6 @@ extern "C" int aaclip_anomaly_map_partials(const float* part, int64_t ld_part, i
   return AACLIP_OK;
 }
 
-extern "C" int aaclip_anomaly_map_fused(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
-                                        const float* T, int batch, int g, int channels, int out_size, int ksize,
-                                        float sigma, float* grid_ws, int* band_counters, float* out,
-                                        void* stream) {
-  AACLIP_REQUIRE(in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16);
-  AACLIP_REQUIRE(levels && T && grid_ws && band_counters && out && batch > 0);
-  AACLIP_REQUIRE(channels == 768 && ld >= channels && ld % 4 == 0);
-  AACLIP_REQUIRE(n_levels >= 1 && n_levels <= kMaxLevels);
-  AACLIP_REQUIRE(g >= 2 && g <= 64 && out_size >= 2 && ceil_div(out_size, kBand) <= kMaxBands);
-  AACLIP_REQUIRE(ksize >= 0 && ksize <= 15 && (ksize == 0 || (ksize % 2 == 1 && ksize / 2 < g)));
-  LevelPtrs lv{};
-  for (int i = 0; i < n_levels; ++i) {
-    AACLIP_REQUIRE(levels[i] != nullptr);
-    lv.p[i] = levels[i];
-  }
-  const Gauss gw = ksize > 0 ? gaussian_weights(ksize, sigma) : Gauss{};
-  const float scale = (float)(g - 1) / (float)(out_size - 1);
-  const int span = (int)(scale * (float)(kBand - 1)) + 4;  // as launch_blur_upsample
-  const int brows = min(g, span);
-  const int xrows = min(g, brows + 2 * (ksize / 2));
-  const size_t lds = (size_t)kFusedWaves * (2 * xrows + brows) * g * sizeof(float);
-  AACLIP_REQUIRE(lds <= 64 * 1024);
-  const int nbands = ceil_div(out_size, kBand);
-  const dim3 grd(g, batch);
-  hipStream_t s = (hipStream_t)stream;
-  const bool f32 = in_dtype == AACLIP_F32, nl4 = n_levels <= 4;
-#define MF_LAUNCH(F, NLM, K)                                                                                     \
-  map_fused_kernel<F, NLM, K><<<grd, 64 * kFusedWaves, lds, s>>>(lv, n_levels, ld, T, g, out_size, ksize, gw,    \
-                                                                 scale, xrows, brows, nbands, grid_ws,           \
-                                                                 band_counters, out)
-#define MF_K(F, NLM)                \
-  if (ksize == 7) MF_LAUNCH(F, NLM, 7);      \
-  else if (ksize == 9) MF_LAUNCH(F, NLM, 9); \
-  else if (ksize == 0) MF_LAUNCH(F, NLM, 0); \
-  else MF_LAUNCH(F, NLM, -1);
-  if (f32) {
-    if (nl4) { MF_K(true, 4) } else { MF_K(true, kMaxLevels) }
-  } else {
-    if (nl4) { MF_K(false, 4) } else { MF_K(false, kMaxLevels) }
-  }
-#undef MF_K
-#undef MF_LAUNCH
-  AACLIP_CHECK_LAUNCH();
-  return AACLIP_OK;
-}
-
 extern "C" int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld, const float* T,
                                   int batch, int n_patch, int channels, int normalize,
                                   float* partial, float* det, float* score, void* stream) {
@@ -813,55 +673,12 @@ extern "C" int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld,
   const int nchunk = ceil_div(n_patch, kDetRows);
   const dim3 grd(nchunk, batch);
   if (in_dtype == AACLIP_F32)
-    map_det_kernel<0, true, 16><<<grd, 1024, 0, (hipStream_t)stream>>>(LevelPtrs{}, ld, det_raw, nullptr, n_patch,
-                                                                       normalize, nullptr, partial, nchunk);
+    map_det_kernel<true><<<grd, 1024, 0, (hipStream_t)stream>>>(ld, det_raw, n_patch, normalize, partial, nchunk);
   else
-    map_det_kernel<0, false, 16><<<grd, 1024, 0, (hipStream_t)stream>>>(LevelPtrs{}, ld, det_raw, nullptr, n_patch,
-                                                                        normalize, nullptr, partial, nchunk);
+    map_det_kernel<false><<<grd, 1024, 0, (hipStream_t)stream>>>(ld, det_raw, n_patch, normalize, partial, nchunk);
   AACLIP_CHECK_LAUNCH();
   det_finalize_kernel<<<batch, 768, 0, (hipStream_t)stream>>>(partial, nchunk, n_patch, T, det,
                                                               score);
-  AACLIP_CHECK_LAUNCH();
-  return AACLIP_OK;
-}
-
-extern "C" int aaclip_anomaly_map_score(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
-                                        const void* det_raw, const float* T, int batch, int g, int channels,
-                                        int out_size, int ksize, float sigma, float* grid_ws, float* partial,
-                                        float* out, float* det, float* score, void* stream) {
-  AACLIP_REQUIRE(in_dtype == AACLIP_F32 || in_dtype == AACLIP_BF16);
-  AACLIP_REQUIRE(levels && det_raw && T && grid_ws && partial && out && score && batch > 0 && g >= 2);
-  AACLIP_REQUIRE(channels == 768 && ld >= channels && ld % 4 == 0);
-  AACLIP_REQUIRE(n_levels >= 1 && n_levels <= kMaxLevels);
-  AACLIP_REQUIRE(blur_upsample_args_ok(1, g, out_size, ksize));  // before map_det_kernel writes anything
-  LevelPtrs lv{};
-  for (int i = 0; i < n_levels; ++i) {
-    AACLIP_REQUIRE(levels[i] != nullptr);
-    lv.p[i] = levels[i];
-  }
-  const int n_patch = g * g;
-  const int nchunk = ceil_div(n_patch, kDetRows);
-  const dim3 grd(nchunk, batch);
-  hipStream_t s = (hipStream_t)stream;
-  const bool f32 = in_dtype == AACLIP_F32;
-#define MD_LAUNCH(NL, W)                                                                                         \
-  (f32 ? map_det_kernel<NL, true, W><<<grd, 64 * W, 0, s>>>(lv, ld, det_raw, T, n_patch, 1, grid_ws, partial, nchunk) \
-       : map_det_kernel<NL, false, W><<<grd, 64 * W, 0, s>>>(lv, ld, det_raw, T, n_patch, 1, grid_ws, partial, nchunk))
-  switch (n_levels) {  // 16 one-row waves while NL levels fit 128 registers (NL <= 6), else 4 waves x 4 rows
-    case 1: MD_LAUNCH(1, 16); break;
-    case 2: MD_LAUNCH(2, 16); break;
-    case 3: MD_LAUNCH(3, 16); break;
-    case 4: MD_LAUNCH(4, 16); break;
-    case 5: MD_LAUNCH(5, 16); break;
-    case 6: MD_LAUNCH(6, 16); break;
-    case 7: MD_LAUNCH(7, 4); break;
-    default: MD_LAUNCH(8, 4); break;
-  }
-#undef MD_LAUNCH
-  AACLIP_CHECK_LAUNCH();
-  const int rc = aaclip_blur_upsample(grid_ws, out, batch, 1, g, out_size, ksize, sigma, 0, stream);
-  if (rc) return rc;
-  det_finalize_kernel<<<batch, 768, 0, s>>>(partial, nchunk, n_patch, T, det, score);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

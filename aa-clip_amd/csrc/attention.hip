@@ -278,100 +278,6 @@ __device__ __forceinline__ void attn_tile_split(const char* kt_lds, const h16x8_
   for (int ks = 0; ks < 2; ++ks) l_acc[1] = mfma16(ones, p1[ks], l_acc[1]);
 }
 
-// Full 64-key tile for two 16-query blocks, speculative exponentials (tiles after the
-// first): both blocks' Kᵀ·Q first, then block 0's p = exp2(S' - m) formed against the
-// CURRENT running max before the deferred-max check -- the exponentials depend only on
-// the scores, so they issue beside block 1's Kᵀ·Q MFMAs instead of waiting for a max
-// tree, a ballot and a branch. Both blocks' lane maxima feed ONE ballot; on its rare
-// taken path each block rescales exactly as attn_tile_split does (a block that does not
-// move gets d = 0: alpha = 1, st - 0, the same bits) and block 0's p is formed again
-// from the shifted scores. On the common path the executed arithmetic is the split
-// tile's, so the results are bit-identical to it. A p formed against a stale max may be
-// +inf (S' - m > 128); it is discarded on that path.
-template <bool H16>
-__device__ __forceinline__ void attn_tile_spec(const char* kt_lds, const h16x8_t<H16> (&qf)[2][2],
-                                               float4_t (&ot)[2][4], float (&m_run)[2], float4_t (&l_acc)[2],
-                                               int g, int c) {
-  using V8 = h16x8_t<H16>;
-  using E = h16_t<H16>;
-  const char* vt_lds = kt_lds + KT * 128;
-  V8 kf[4][2];
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) kf[kb][ks] = *(const V8*)(kt_lds + swz(kb * 16 + c, ks * 4 + g));
-  auto qk = [&](int qb, float4_t (&st)[4]) {
-    const float nm = -m_run[qb];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) st[kb] = float4_t{nm, nm, nm, nm};
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) st[kb] = mfma16(kf[kb][ks], qf[qb][ks], st[kb]);
-  };
-  auto expo = [&](const float4_t (&st)[4], V8 (&pf)[2]) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      V8 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] = (E)__builtin_amdgcn_exp2f(st[2 * ks][i]);
-        v[4 + i] = (E)__builtin_amdgcn_exp2f(st[2 * ks + 1][i]);
-      }
-      pf[ks] = v;
-    }
-  };
-  auto rescale = [&](int qb, float4_t (&st)[4], float mx) {
-    mx = max_over_groups(mx);
-    const float d = mx > kRescaleLog2 ? mx : 0.f;
-    m_run[qb] += d;
-    const float alpha = __builtin_amdgcn_exp2f(-d);
-    l_acc[qb][0] *= alpha;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ot[qb][db][e] *= alpha;
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) st[kb][i] -= d;
-  };
-  float4_t s0[4], s1[4];
-  V8 p0[2], p1[2];
-  qk(0, s0);
-  qk(1, s1);
-  expo(s0, p0);
-  // pin the speculative exponentials ahead of the branch (hipcc would otherwise sink
-  // them into the not-taken path, behind the ballot)
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(p0[ks]));
-  const float mx0 = tile_lane_max<4>(s0), mx1 = tile_lane_max<4>(s1);
-  if (__builtin_amdgcn_ballot_w64(mx0 > kRescaleLog2 || mx1 > kRescaleLog2) != 0) {
-    rescale(0, s0, mx0);
-    rescale(1, s1, mx1);
-    expo(s0, p0);
-  }
-  expo(s1, p1);
-  const V8 ones = {(E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f, (E)1.f};
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) l_acc[0] = mfma16(ones, p0[ks], l_acc[0]);
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int qq = c >> 2, pp = c & 3;
-      const int chunk = db * 2 + (pp >> 1);
-      const int r0 = ks * 32 + 4 * g + qq;
-      const short4_t lo = tr_read(vt_lds + swz(r0, chunk) + (pp & 1) * 8);
-      const short4_t hi = tr_read(vt_lds + swz(r0 + 16, chunk) + (pp & 1) * 8);
-      const V8 vf = __builtin_bit_cast(V8, short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-      ot[0][db] = mfma16(vf, p0[ks], ot[0][db]);
-      ot[1][db] = mfma16(vf, p1[ks], ot[1][db]);
-    }
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) l_acc[1] = mfma16(ones, p1[ks], l_acc[1]);
-}
-
 #ifndef ATTN_STAGES
 #define ATTN_STAGES 3  // K/V ring depth (LDS: ATTN_STAGES x 16 KiB per workgroup)
 #endif
@@ -538,12 +444,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
   for (; t < nfull; ++t) {
     const bool deep = advance();
     if (active) {
-      if constexpr (SPLIT == 2 && QB == 2) {
-        if (t == 0)
-          attn_tile_split<H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, g, c, true);
-        else
-          attn_tile_spec<H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, g, c);
-      } else if constexpr (SPLIT == 1 && QB == 2)
+      if constexpr (SPLIT == 1 && QB == 2)
         attn_tile_split<H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, g, c, t == 0);
       else
         attn_tile<4, QB, false, H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g,
@@ -837,437 +738,12 @@ __global__ __launch_bounds__(256, 2) void attn_f32_kernel(const float* __restric
   }
 }
 
-// ======================= 32x32x16 MFMA kernel with a cross-tile software pipeline
-// Workgroup = 4 waves x 32 queries of one (image, head), 64-key K/V tiles in a 3-slot
-// LDS-DMA ring, ONE barrier per tile. Per wave and tile t the loop body is one
-// straight-line block:
-//   phase A: S(t+1)^T = K(t+1) . Q^T on v_mfma_f32_32x32x16 (8 MFMAs, independent of
-//            the softmax) beside P(t) = exp2(S(t)^T - m) -> bf16 (32 v_exp, 16 cvt);
-//   phase B: O^T += V(t)^T . P(t)^T (8 MFMAs; V^T by ds_read_b64_tr_b16) and the row
-//            sums l += 1 . P(t)^T (4 MFMAs) beside the max tree of S(t+1) and the
-//            deferred-max check that covers it (rescale path rare, as attn_tile).
-// 32x32x16 instead of 16x16x32: an MFMA holds vector issue 8 of its 32 cycles instead
-// of 8 of 16, so the 20 MFMAs of a wave-tile leave ~480 issue cycles for the ~420 of
-// softmax VALU (the 16x16 kernel's 36 MFMAs left the loop issue-bound: 764 issue
-// cycles per 576 MFMA cycles), and the pipeline hands the VALU of tile t
-// work that does not wait on tile t's own MFMA results.
-// Layouts (cdna_hip_programming.md §3): S^T[key][q] = K . Q^T with A = K rows (lane r =
-// key, k = d), B = Q^T (lane r = query): lane l holds query l&31, keys
-// 32kb + 8(i>>2) + 4(l>>5) + (i&3) in register i of block kb. Registers 8s..8s+7,
-// packed to 16 bits, are P^T's B fragment for the 16-key step s with that key
-// permutation; the V^T A fragment takes the same keys: two transposing reads of 4
-// consecutive keys (rows 16s + 4h.. and 16s + 8 + 4h..) of the row-major V tile.
-// The softmax arithmetic is attn_tile's (log2 domain, Q prescaled, accumulator
-// initialised to -m, deferred max with the 2^8 bound, bf16/fp16-rounded p for both
-// numerator and denominator); only the MFMA shape (summation order) differs.
-typedef __attribute__((ext_vector_type(16))) float f32x16_t;
-
-__device__ __forceinline__ f32x16_t mfma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x16_t mfma32(const f16x8_t& a, const f16x8_t& b, const f32x16_t& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
-
-// LDS reads of the pipelined loop as inline asm: the compiler's waitcnt pass cannot see
-// that a ds_read_b64_tr_b16 builtin does not alias the in-flight LDS-DMA ring, and puts a
-// vmcnt(0) before the first one of every tile (draining the prefetch of tile t+3); asm
-// reads carry their own lgkmcnt waits, tied to the registers they produce (LDS reads
-// complete in issue order, so "all but the N youngest" is exact).
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-template <int OFF>
-__device__ __forceinline__ short8_t lds_b128(uint32_t a) {
-  short8_t v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
-  return v;
-}
-template <int OFF>
-__device__ __forceinline__ short4_t lds_tr(uint32_t a) {
-  short4_t v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
-  return v;
-}
-template <int N, typename T>
-__device__ __forceinline__ void lgkm_wait(T& v) {
-  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "i"(N));
-}
-template <int N>
-__device__ __forceinline__ void lgkm_wait(short4_t (&d)[4]) {
-  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]) : "i"(N));
-}
-
-// OCC: workgroups per CU the registers are sized for (2: 4-slot ring, tiles t+1..t+3 in
-// flight; 3: 3-slot ring, ~25 VGPRs spilled -- measured); MSUM: row sums
-// by a ones-operand MFMA (4 per tile, bf16-rounded p like the numerator) instead of f32
-// VALU adds of the exponentials.
-template <bool H16, int OCC, bool MSUM>
-__global__ __launch_bounds__(256, OCC) void attn32_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
-                                                        int batch, int N, int H, int flags) {
-  using V8 = h16x8_t<H16>;
-  using E = h16_t<H16>;
-  constexpr int NS = OCC == 2 ? 4 : 3, SLOT = 2 * KT * 128;  // [slot][K|V][64 rows][128 B]
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, hh = lane >> 5;
-  // XCD-aware remap, query tiles of one (image, head) consecutive (as attn_bf16_kernel)
-  const int nq = (N + 127) / 128;
-  const int nwg = gridDim.x;
-  const int xcd = blockIdx.x & 7, qd = nwg >> 3, rd = nwg & 7;
-  const int wgid = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (blockIdx.x >> 3);
-  const int qtile = wgid % nq;
-  const int bh = wgid / nq;
-  const int b = bh / H, h = bh % H;
-  const int HDt = H * HD_;
-  const int64_t ld = 3 * (int64_t)HDt;
-  const uint16_t* base = qkv + (size_t)b * N * ld + h * HD_;
-  const int q0 = qtile * 128 + wid * 32;
-  const bool active = q0 < N;
-  const int q = min(q0 + r, N - 1);
-
-  // Q^T fragments (B of K.Q^T): lane holds Q[q][16 ks + 8 hh .. +7]
-  V8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const V8*)(base + (size_t)q * ld + 16 * ks + 8 * hh);
-  if (!(flags & AACLIP_ATTN_Q_PRESCALED)) {
-    constexpr float sl2 = 0.125f * 1.4426950408889634f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qf[ks][e] = (E)((float)qf[ks][e] * sl2);
-  }
-
-  // K/V DMA: wave w moves 8-row pieces w and w+4 of the K and of the V tile into a
-  // lane-linear image whose physical 16-B chunk p of row `row` holds logical chunk
-  // p ^ kswz(row) (K) / p ^ vswz(row) (V). The 32x32 operand reads need their own XORs
-  // (the 16x16 kernel's row & 7 is 2-way conflicted here, PMC: 5.9 M conflict cycles):
-  // K's ds_read_b128 lane groups ({0-3,12-15,20-27}, ...: rows r of one parity, one
-  // logical chunk) hit distinct banks with (row >> 1) & 7; V's transposed reads (a
-  // 32-lane half: 4 consecutive rows x 4 chunks x 2 halves) with bit 2 flipped on rows
-  // 2, 3 mod 4.
-  const int64_t head0 = (int64_t)b * N * ld + h * HD_;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(qkv + head0), 0,
-                                                    (int)(((int64_t)batch * N * ld - head0) * 2), 0x00020000);
-  auto kswz = [](int row) { return (row >> 1) & 7; };
-  auto vswz = [](int row) { return ((row >> 1) & 1) << 2; };
-  int koff[2], voff[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (i * 4 + wid) * 8 + (lane >> 3);
-    koff[i] = (int)(row * ld + HDt + ((lane & 7) ^ kswz(row)) * 8) * 2;
-    voff[i] = (int)(row * ld + 2 * HDt + ((lane & 7) ^ vswz(row)) * 8) * 2;
-  }
-  const int row_bytes = (int)ld * 2;
-  auto stage = [&](int t, int slot) {
-    char* kb = smem + slot * SLOT;
-    const int so = t * KT * row_bytes;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(kb + (i * 4 + wid) * 1024), 16, koff[i], so, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(kb + KT * 128 + (i * 4 + wid) * 1024), 16, voff[i], so,
-                                               0, 0);
-    }
-  };
-  // per-lane LDS read addresses (slot 0; + slot * SLOT per tile):
-  // K frag (kb, ks): row 32 kb + r, logical chunk 2 ks + hh; kb = 1 is +4096 (same XOR)
-  const uint32_t lds0 = lds_addr(smem);
-  uint32_t ka[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) ka[ks] = lds0 + r * 128 + (((2 * ks + hh) ^ kswz(r)) << 4);
-  // V^T frag: 16-lane group G = lane >> 4 reads 4 rows row0 + (lane & 15) / 4 of columns
-  // 32 db + 16 (G & 1) + 4 (lane & 3) .. +3; row0 = 32 kb + 16 st + 8 j4 + 4 hh = 0 mod 4, so
-  // the row's XOR term vswz(row0 + qq) is the same for every (kb, st, j4): immediates
-  const int qq = (lane & 15) >> 2, gcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  uint32_t va[2];
-#pragma unroll
-  for (int db = 0; db < 2; ++db) {
-    const int row = 4 * hh + qq, col = 32 * db + gcol;
-    va[db] = lds0 + KT * 128 + row * 128 + (((col >> 3) ^ vswz(row)) << 4) + (col & 7) * 2;
-  }
-
-  const int tail_keys = N % KT;
-  const bool tail_inline = (flags & AACLIP_ATTN_CAUSAL) == 0 && tail_keys <= 8;
-  const int nt = N / KT;  // full tiles (the caller guarantees tail_inline)
-  f32x16_t o[2], splat, sa[2], sb[2];  // sa / sb: the two score sets
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    o[0][i] = 0.f;
-    o[1][i] = 0.f;
-  }
-  // row sums: this lane's half of the query's keys, f32 adds of the exponentials (two
-  // chains); the halves are combined at the end. (A ones-operand 32x32 MFMA would cost 4
-  // MFMAs = 128 matrix cycles per tile for one useful row of 32.)
-  float l0 = 0.f, l1 = 0.f;
-  float m_run = 0.f;
-  f32x16_t l_acc;  // MSUM: every row of it holds the sums
-  V8 ones;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) l_acc[i] = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (E)1.f;
-
-  auto lane_max = [&](const f32x16_t (&s)[2]) {
-    float a = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]);
-#pragma unroll
-    for (int i = 3; i < 15; i += 2) a = fmaxf(fmaxf(a, s[0][i]), s[0][i + 1]);
-    float c = fmaxf(fmaxf(s[1][0], s[1][1]), s[1][2]);
-#pragma unroll
-    for (int i = 3; i < 15; i += 2) c = fmaxf(fmaxf(c, s[1][i]), s[1][i + 1]);
-    return fmaxf(fmaxf(a, s[0][15]), fmaxf(c, s[1][15]));
-  };
-  auto half_max = [&](float v) {  // max with the other half-wave's keys of the same query
-    auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(x[0]), __uint_as_float(x[1]));
-  };
-  auto pack = [&](const f32x16_t& s, int st) {  // registers 8 st .. 8 st + 7 -> exp2 -> 16-bit B fragment
-    V8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (E)__builtin_amdgcn_exp2f(s[8 * st + j]);
-    return v;
-  };
-  // S(t)^T = K(t) . Q^T (+ c) from slot `slot`, with up to 3 of P's fragment packs
-  // placed between the MFMAs (phase A)
-  auto read_k = [&](uint32_t so, short8_t (&kf)[2][4]) {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) kf[0][ks] = lds_b128<0>(ka[ks] + so);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) kf[1][ks] = lds_b128<4096>(ka[ks] + so);
-  };
-  auto read_k_half = [&](uint32_t so, short8_t (&kf)[4], auto kb) {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) kf[ks] = lds_b128<4096 * decltype(kb)::value>(ka[ks] + so);
-  };
-
-  // prologue: tiles 0..2 in flight, S(0) with a zero accumulator, the running max from
-  // tile 0 (every query has 64 valid keys there), S(0) -= m
-  stage(0, 0);
-  if (nt > 1) stage(1, 1);
-  if (NS == 4 && nt > 2) {
-    stage(2, 2);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if (active) {
-    short8_t kf[2][4];
-    read_k(0, kf);
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) lgkm_wait<0>(kf[kb][ks]);  // tied: no MFMA reads them earlier
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sa[kb][i] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) sa[kb] = mfma32(__builtin_bit_cast(V8, kf[kb][ks]), qf[ks], sa[kb]);
-    }
-    m_run = half_max(lane_max(sa));
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sa[kb][i] -= m_run;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) splat[i] = -m_run;
-  }
-
-  // one tile: P(t) from sc, S(t+1) into sn (the score sets swap roles every tile; the loop
-  // is unrolled by two so they stay in fixed registers, no copies)
-  auto step = [&](int t, int cur, f32x16_t (&sc)[2], f32x16_t (&sn)[2]) {
-    const int nxt = cur == NS - 1 ? 0 : cur + 1;
-    const int ahead = NS - 1;  // tiles issued ahead of t
-    const bool deep = t + ahead < nt;
-    if (deep) stage(t + ahead, cur == 0 ? NS - 1 : cur - 1);
-    if (active) {
-      const bool more = t + 1 < nt;
-      // phase A: S(t+1) = K(t+1) . Q^T (8 MFMAs, slot nxt: a stale slot after the last
-      // tile, result unused -- the block stays straight-line) beside 2.5 of P(t)'s 4 packs;
-      // phase B: O^T += V(t)^T . P(t)^T, l += 1 . P^T (12 MFMAs; V^T reads one group ahead)
-      // beside the last 1.5 packs and S(t+1)'s max tree. sched_barrier fences pin each
-      // group's VALU next to its MFMA (hipcc otherwise bunches the waits and the VALU).
-      short8_t kf[2][4];
-      read_k_half(nxt * SLOT, kf[0], std::integral_constant<int, 0>{});
-      V8 pf[2][2];
-      auto half = [&](V8& v, const f32x16_t& sv, int st, int hf) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float e = __builtin_amdgcn_exp2f(sv[8 * st + 4 * hf + j]);
-          v[4 * hf + j] = (E)e;
-          if constexpr (!MSUM) {
-            if (j & 1) l1 += e; else l0 += e;
-          }
-        }
-      };
-#define FENCE() __builtin_amdgcn_sched_barrier(0)
-#define QK_MFMA(KB, KS, N)                                                                                 \
-  lgkm_wait<N>(kf[KB][KS]);                                                                                \
-  sn[KB] = mfma32(__builtin_bit_cast(V8, kf[KB][KS]), qf[KS], KS == 0 ? splat : sn[KB]);
-      half(pf[0][0], sc[0], 0, 0);  // covers the K reads' LDS latency
-      half(pf[0][0], sc[0], 0, 1);
-      FENCE();
-      QK_MFMA(0, 0, 3)
-      FENCE();
-      QK_MFMA(0, 1, 2)
-      read_k_half(nxt * SLOT, kf[1], std::integral_constant<int, 1>{});
-      half(pf[0][1], sc[0], 1, 0);
-      FENCE();
-      QK_MFMA(0, 2, 5)
-      half(pf[0][1], sc[0], 1, 1);
-      FENCE();
-      QK_MFMA(0, 3, 4)
-      FENCE();
-      QK_MFMA(1, 0, 3)
-      half(pf[1][0], sc[1], 0, 0);
-      FENCE();
-      QK_MFMA(1, 1, 2)
-      FENCE();
-      QK_MFMA(1, 2, 1)
-      FENCE();
-      QK_MFMA(1, 3, 0)
-      FENCE();
-#undef QK_MFMA
-      const uint32_t vs = cur * SLOT;
-      short4_t vr[2][4];  // [buffer][db * 2 + j4]
-      auto read_v = [&](auto kbst, short4_t (&d)[4]) {
-        constexpr int off = 1024 * decltype(kbst)::value;  // (32 kb + 16 st) rows * 128 B
-        d[0] = lds_tr<off>(va[0] + vs);
-        d[1] = lds_tr<off + 1024>(va[0] + vs);
-        d[2] = lds_tr<off>(va[1] + vs);
-        d[3] = lds_tr<off + 1024>(va[1] + vs);
-      };
-      auto pv = [&](const short4_t (&d)[4], const V8& p) {
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const short4_t lo = d[2 * db], hi = d[2 * db + 1];
-          o[db] = mfma32(__builtin_bit_cast(V8, short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}), p,
-                         o[db]);
-        }
-        if constexpr (MSUM) l_acc = mfma32(ones, p, l_acc);
-      };
-      read_v(std::integral_constant<int, 0>{}, vr[0]);  // (kb, st) = (0, 0): rows 0..
-      read_v(std::integral_constant<int, 2>{}, vr[1]);  // (0, 1): rows 16..
-      half(pf[1][0], sc[1], 0, 1);
-      FENCE();
-      lgkm_wait<4>(vr[0]);
-      pv(vr[0], pf[0][0]);
-      read_v(std::integral_constant<int, 4>{}, vr[0]);  // (1, 0): rows 32..
-      half(pf[1][1], sc[1], 1, 0);
-      FENCE();
-      lgkm_wait<4>(vr[1]);
-      pv(vr[1], pf[0][1]);
-      read_v(std::integral_constant<int, 6>{}, vr[1]);  // (1, 1): rows 48..
-      half(pf[1][1], sc[1], 1, 1);
-      FENCE();
-      lgkm_wait<4>(vr[0]);
-      pv(vr[0], pf[1][0]);
-      const float mx = lane_max(sn);
-      FENCE();
-      lgkm_wait<0>(vr[1]);
-      pv(vr[1], pf[1][1]);
-#undef FENCE
-      if (more && __builtin_amdgcn_ballot_w64(mx > kRescaleLog2) != 0) {  // rare: the running max moves
-        const float fm = half_max(mx);
-        const float d = fm > kRescaleLog2 ? fm : 0.f;
-        m_run += d;
-        const float alpha = __builtin_amdgcn_exp2f(-d);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          o[0][i] *= alpha;
-          o[1][i] *= alpha;
-          sn[0][i] -= d;
-          sn[1][i] -= d;
-          splat[i] = -m_run;
-        }
-        l0 *= alpha;
-        l1 *= alpha;
-        if constexpr (MSUM) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) l_acc[i] *= alpha;
-        }
-      }
-    }
-    // tile t+2 landed (this wave's pieces; with 4 slots t+3's stay in flight), then every wave's
-    if (NS == 4 && deep)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    return nxt;
-  };
-  int cur = 0;  // slot of tile t
-  for (int t = 0; t < nt; t += 2) {
-    cur = step(t, cur, sa, sb);
-    if (t + 1 < nt) cur = step(t + 1, cur, sb, sa);
-  }
-
-
-
-  if (!active) return;
-  // the query's row sum: this half-wave's keys + the other half's (same bits in both)
-  float l_sum = l0 + l1;
-  if constexpr (MSUM) l_sum = l_acc[0];
-  else {
-    auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_sum), __float_as_uint(l_sum), false, false);
-    l_sum = __uint_as_float(x[0]) + __uint_as_float(x[1]);
-  }
-  if (tail_inline && tail_keys > 0) {  // the 1-key tail of 577 / 1025: exact per-key updates
-    const uint16_t* kt_g = base + HDt;
-    const uint16_t* vt_g = base + 2 * HDt;
-    for (int j = N - tail_keys; j < N; ++j) {
-      const uint16_t* kr = kt_g + (size_t)j * ld;
-      float sp = 0.f;  // this lane's 32 of the 64 dims
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const V8 kf = *(const V8*)(kr + 16 * ks + 8 * hh);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sp = fmaf((float)qf[ks][e], (float)kf[e], sp);
-      }
-      auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(sp), __float_as_uint(sp), false, false);
-      sp = __uint_as_float(x[0]) + __uint_as_float(x[1]);
-      const float mn = fmaxf(m_run, sp);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - mn), p = __builtin_amdgcn_exp2f(sp - mn);
-      m_run = mn;
-      l_sum = fmaf(l_sum, alpha, p);
-      const uint16_t* vr = vt_g + (size_t)j * ld;
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) {  // d = 32 db + 8 k4 + 4 hh + i
-          const uint2 w = *(const uint2*)(vr + 32 * db + 8 * k4 + 4 * hh);
-          const float vv[4] = {h16_to_f32<H16>((uint16_t)(w.x & 0xffff)), h16_to_f32<H16>((uint16_t)(w.x >> 16)),
-                               h16_to_f32<H16>((uint16_t)(w.y & 0xffff)), h16_to_f32<H16>((uint16_t)(w.y >> 16))};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o[db][4 * k4 + i] = fmaf(o[db][4 * k4 + i], alpha, p * vv[i]);
-        }
-    }
-  }
-  // O[q][d]: the lane holds d = 32 db + 8 k4 + 4 hh + i; the two half-waves' 8-byte pieces
-  // of column groups k4, k4 + 1 are exchanged with v_permlane32_swap so every lane stores 16
-  // contiguous bytes (half 0: columns 8 k4 .. +7, half 1: 8 (k4 + 1) .. +7)
-  const float inv = 1.0f / l_sum;
-  const bool qok = q0 + r < N;
-  uint16_t* op = out + ((size_t)b * N + min(q0 + r, N - 1)) * HDt + h * HD_;
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int k4 = 0; k4 < 4; k4 += 2) {
-      uint32_t a0 = pack_h16x2<H16>(o[db][4 * k4] * inv, o[db][4 * k4 + 1] * inv);
-      uint32_t a1 = pack_h16x2<H16>(o[db][4 * k4 + 2] * inv, o[db][4 * k4 + 3] * inv);
-      uint32_t b0 = pack_h16x2<H16>(o[db][4 * k4 + 4] * inv, o[db][4 * k4 + 5] * inv);
-      uint32_t b1 = pack_h16x2<H16>(o[db][4 * k4 + 6] * inv, o[db][4 * k4 + 7] * inv);
-      const auto x = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-      const auto y = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-      if (qok) *(uint4*)(op + 32 * db + 8 * k4 + 8 * hh) = uint4{x[0], y[0], x[1], y[1]};
-    }
-}
-
 // 1 = 4 waves x 32 queries (3-stage ring, 3 workgroups per CU), 2 = 2 waves x 64
 // queries (2-stage ring, 4 workgroups per CU: half the LDS bytes per FLOP), 3 = 1
-// with the phase-split full tile (attn_tile_split: 3-6 % faster, the default), 4 = 3
-// with speculative exponentials after tile 0 (attn_tile_spec, same bits)
+// with the phase-split full tile (attn_tile_split: 3-6 % faster, the default). Removed
+// in round 5 after measuring slower or equal (round-4 history): 4 = speculative
+// exponentials (same bits, equal), 5-7 = the 32x32x16 cross-tile pipelined kernel
+// (10 % slower at 2 workgroups per CU, spills at 3).
 constexpr int kAttnDefault = 3;
 int g_attn_variant = 0;
 
@@ -1281,7 +757,7 @@ void launch_attn(const uint16_t* q, uint16_t* o, int batch, int seq, int heads, 
 }  // namespace
 
 extern "C" int aaclip_set_attn_variant(int variant) {
-  AACLIP_REQUIRE(variant >= 0 && variant <= 7);
+  AACLIP_REQUIRE(variant >= 0 && variant <= 3);
   g_attn_variant = variant;
   return AACLIP_OK;
 }
@@ -1303,26 +779,13 @@ extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch
     const uint16_t* q = (const uint16_t*)qkv;
     uint16_t* o = (uint16_t*)out;
     uint8_t* mx = dtype == AACLIP_FP8 ? (uint8_t*)out_mx : nullptr;
-    // the 32x32 pipelined kernel: non-causal, a key tail of at most 8 (577 / 1025 tokens),
-    // at least one full tile, 16-bit output
-    const bool k32 = v >= 5 && !(flags & AACLIP_ATTN_CAUSAL) && seq % KT <= 8 && seq >= KT && !mx;
-    if (k32) {  // 5: 2 WG/CU + MFMA row sums, 6: 2 WG/CU + VALU row sums, 7: 3 WG/CU + VALU row sums
-#define A32(H, OCC, MS) attn32_kernel<H, OCC, MS><<<(unsigned)nwg, 256, 0, s>>>(q, o, batch, seq, heads, flags)
-      if (dtype == AACLIP_F16) {
-        if (v == 5) A32(true, 2, true); else if (v == 6) A32(true, 2, false); else A32(true, 3, false);
-      } else {
-        if (v == 5) A32(false, 2, true); else if (v == 6) A32(false, 2, false); else A32(false, 3, false);
-      }
-#undef A32
-    } else if (dtype == AACLIP_F16) {
+    if (dtype == AACLIP_F16) {
       if (v == 2) launch_attn<true, 4, 2, 2>(q, o, batch, seq, heads, flags, nullptr, 0, s);
       else if (v == 3) launch_attn<true, 2, 4, ATTN_STAGES, 1>(q, o, batch, seq, heads, flags, nullptr, 0, s);
-      else if (v == 4) launch_attn<true, 2, 4, ATTN_STAGES, 2>(q, o, batch, seq, heads, flags, nullptr, 0, s);
       else launch_attn<true, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, nullptr, 0, s);
     } else {
       if (v == 2) launch_attn<false, 4, 2, 2>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
       else if (v == 3) launch_attn<false, 2, 4, ATTN_STAGES, 1>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
-      else if (v == 4) launch_attn<false, 2, 4, ATTN_STAGES, 2>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
       else launch_attn<false, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
     }
   } else {

@@ -804,18 +804,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
 // Loads past the last K-step re-read its columns into regions nobody reads again,
 // so the vmcnt arithmetic stays uniform. Operands via buffer descriptors (rows >= M
 // read as zero; outputs dropped by the epilogue's bound check).
-// PERSIST: one workgroup per CU walks tiles blockIdx.x, + gridDim.x, ... (same XCD:
-// the grid is a multiple of 8 or the whole tile set). The K-step index runs on
-// across tiles: the loads the last two K-steps of tile t would issue past its end
-// (the phantom loads) fetch tile t+1's K-steps 0-1 instead, so tile t+1 has no
-// prologue and its first regions land while tile t's epilogue runs. The epilogue's
-// S stores then sit in the in-order vmcnt stream between those DMAs and the next
-// ones: the four phases of tile t+1's first K-step wait vmcnt(8 + S) (S counted per
-// epilogue case; 0 = strict for edge tiles and the run-time-flag epilogues), so the
-// stores drain under four MFMA phases before vmcnt(8) requires them.
+// (A persistent form -- one workgroup per CU walking tiles, the next tile's first
+// K-steps fetched by the phantom loads under the epilogue -- measured -1.0 % in the C2
+// step and was removed in round 5; it is in the round-4 history, family 5.)
 // SCORES: the instantiation for aaclip_gemm_scores (OUTM 3 epilogue only), so the
 // anomaly-map partials path adds no registers to the block-GEMM instantiations.
-template <bool H16, bool PERSIST, bool SCORES = false>
+template <bool H16, bool SCORES = false>
 __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   using V8 = h16x8_t<H16>;
   constexpr int BM = 256, BN = 256, TM = 128, TN = 64, RM = 8, RN = 4;
@@ -827,7 +821,6 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
-  const int ntiles = a.tiles_m * a.tiles_n;
   const auto ars = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)((uint32_t)a.M * (uint32_t)a.lda * 2u),
                                                      0x00020000);
   const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, (int)((uint32_t)a.N * (uint32_t)a.ldw * 2u),
@@ -840,18 +833,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   auto w_vo_of = [&](int n0) { return ((n0 + ((prow >> 5) & 1) * 64 + (prow & 31)) * (int)a.ldw + pchunk) * 2; };
   const int a_row = (int)a.lda * 2, w_row = (int)a.ldw * 2;  // bytes per row
   const int nk = a.K / 64;
-  int tile = blockIdx.x;
   int tm, tn;
-  tile_coords(tile, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
-  int a_vo = a_vo_of(tm * BM), w_vo = w_vo_of(tn * BN);
-  int a_vo_next = a_vo, w_vo_next = w_vo;  // the next tile's, when there is one
-  bool has_next = false;
+  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
+  const int avo = a_vo_of(tm * BM), wvo = w_vo_of(tn * BN);
   // region r of K-step kt into stage kt&1 (r: 0 = A0, 1 = A1, 2 = B0, 3 = B1); kt >= nk
-  // is the next tile's K-step kt - nk (PERSIST) or a phantom re-read of the last one
+  // is a phantom re-read of the last one
   auto issue = [&](int r, int kt) {
-    const bool nxt = PERSIST && kt >= nk && has_next;
-    const int kc = (nxt ? kt - nk : min(kt, nk - 1)) * 128;
-    const int avo = nxt ? a_vo_next : a_vo, wvo = nxt ? w_vo_next : w_vo;
+    const int kc = min(kt, nk - 1) * 128;
     char* dst = smem + (kt & 1) * STAGE + r * REGION;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -878,7 +866,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   // the tile's 256 bias values into LDS behind the ring (one 1-KiB DMA by wave 0, retired by
   // the prologue's vmcnt(8) as the oldest op): the epilogue reads them from LDS instead of
   // waiting out a global-load round trip at its start
-  const bool lds_bias = !PERSIST && !SCORES && (a.epi & AACLIP_EPI_BIAS);
+  const bool lds_bias = !SCORES && (a.epi & AACLIP_EPI_BIAS);
   if (lds_bias && wid == 0) {
     const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)a.bias, 0, (int)((uint32_t)a.N * 4u), 0x00020000);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, LDS_PTR(smem + 2 * STAGE), 16, (tn * BN + 4 * lane) * 4, 0, 0, 0);
@@ -920,19 +908,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       for (int kk = 0; kk < 2; ++kk)
         bfr[q][j][kk] = *(const V8*)(st + q * REGION + b_rd[kk] + j * 2048);
   };
-  // phase-end wait: vmcnt(8), or vmcnt(8 + S) in the first K-step after an epilogue of S stores
-  auto ph_wait = [&](int S) {
-    if (!PERSIST || S == 0)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (S == 16)
-      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-    else if (S == 32)
-      asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(56)" ::: "memory");
-  };
-#define PH_SYNC_MFMA(QA, QB, S)                              \
-  ph_wait(S);                                                \
+#define PH_SYNC_MFMA(QA, QB)                                 \
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");           \
   __builtin_amdgcn_s_barrier();                              \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
   __builtin_amdgcn_sched_barrier(0);                         \
@@ -942,110 +919,73 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
 
   const bool bf16_out = a.out_dtype != AACLIP_F32;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
-  int s_prev = 0;  // stores the previous tile's epilogue left in the vmcnt stream (0 = none / unknown)
-  // diagnostic stamps (variant bit 11, non-persistent launches): shader-clock s_memtime at
-  // kernel start, main-loop end, epilogue issued, epilogue stores complete -> a.aux
-  const bool stamp = !PERSIST && (a.dbg & 4) && a.aux && !(a.epi & AACLIP_EPI_AUX_BF16);
+  // diagnostic stamps (variant bit 11): shader-clock s_memtime at kernel start, main-loop
+  // end, epilogue issued, epilogue stores complete -> a.aux
+  const bool stamp = (a.dbg & 4) && a.aux && !(a.epi & AACLIP_EPI_AUX_BF16);
   uint64_t ts[4] = {0, 0, 0, 0};
   if (stamp) ts[0] = __builtin_amdgcn_s_memtime();
-  for (;;) {
-    const int m0 = tm * BM, n0 = tn * BN;
-    int tm_n = 0, tn_n = 0;
-    if constexpr (PERSIST) {
-      has_next = tile + (int)gridDim.x < ntiles;
-      if (has_next) {
-        tile_coords(tile + (int)gridDim.x, a.tiles_m, a.tiles_n, tm_n, tn_n, a.group_m);
-        a_vo_next = a_vo_of(tm_n * BM);
-        w_vo_next = w_vo_of(tn_n * BN);
-      }
-    }
+  const int m0 = tm * BM, n0 = tn * BN;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * STAGE;
+    // P1: A0 x B0
+    read_b(st, 0);
+    read_a(st, 0);
+    issue(3, kt + 1);
+    PH_SYNC_MFMA(0, 0)
+    // P2: A0 x B1
+    read_b(st, 1);
+    issue(1, kt + 1);
+    PH_SYNC_MFMA(0, 1)
+    // P3: A1 x B1
+    read_a(st, 1);
+    issue(0, kt + 2);
+    PH_SYNC_MFMA(1, 1)
+    // P4: A1 x B0
+    issue(2, kt + 2);
+    PH_SYNC_MFMA(1, 0)
+  }
+  // both wave rows run the epilogue together (row 0 waits out row 1's last phase)
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // the epilogue's LDS slot writes stay behind that barrier
+  const int mw = m0 + wr * TM, nw = n0 + wc * TN;
+  const float* lbp = (const float*)(smem + 2 * STAGE) - n0;  // staged bias, by column
+  // the epilogue's per-wave 4-KiB LDS slot: regions A1 / B1 of the last K-step's stage,
+  // whose last reads (P3 / P2) every wave finished before the barrier above and which
+  // no phantom DMA targets (those fill the other stage and this stage's A0 / B0)
+  char* slot = smem + ((nk - 1) & 1) * STAGE + (wr ? 3 : 1) * REGION + wc * 4096;
+  if (stamp) ts[1] = __builtin_amdgcn_s_memtime();
+  if (a.dbg & 1) {
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
-      const char* st = smem + (kt & 1) * STAGE;
-      const int S = kt == 0 ? s_prev : 0;
-      // P1: A0 x B0
-      read_b(st, 0);
-      read_a(st, 0);
-      issue(3, kt + 1);
-      PH_SYNC_MFMA(0, 0, S)
-      // P2: A0 x B1
-      read_b(st, 1);
-      issue(1, kt + 1);
-      PH_SYNC_MFMA(0, 1, S)
-      // P3: A1 x B1
-      read_a(st, 1);
-      issue(0, kt + 2);
-      PH_SYNC_MFMA(1, 1, S)
-      // P4: A1 x B0
-      issue(2, kt + 2);
-      PH_SYNC_MFMA(1, 0, S)
-    }
-    // both wave rows run the epilogue together (row 0 waits out row 1's last phase);
-    // row 1 re-takes its one-barrier lag before the next tile
-    if (wr == 0) __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");  // the epilogue's LDS slot writes stay behind that barrier
-    const int mw = m0 + wr * TM, nw = n0 + wc * TN;
-    const float* lbp = (const float*)(smem + 2 * STAGE) - n0;  // staged bias, by column
-    // the epilogue's per-wave 4-KiB LDS slot: regions A1 / B1 of the last K-step's stage,
-    // whose last reads (P3 / P2) every wave finished before the barrier above and which
-    // no phantom DMA targets (those fill the other stage and this stage's A0 / B0)
-    char* slot = smem + ((nk - 1) & 1) * STAGE + (wr ? 3 : 1) * REGION + wc * 4096;
-    // S for the next tile's first K-step: a LOWER bound on the VMEM ops this epilogue
-    // issues between the next tile's prefetched regions and its own next DMA (stores;
-    // the bias / residual loads only add to it). Edge tiles skip whole row groups: 0.
-    const bool full = m0 + BM <= a.M;
-    s_prev = 0;
-    if (stamp) ts[1] = __builtin_amdgcn_s_memtime();
-    if (a.dbg & 1) {
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
-    } else if constexpr (SCORES) {  // seg/det proj -> map partials (no stores to overlap)
-      if (key == AACLIP_EPI_LEAKY)
-        wave_epilogue<RM, RN, 3, AACLIP_EPI_LEAKY, 0, H16>(a, acc, mw, nw, lane);
-      else
-        wave_epilogue<RM, RN, 3, 0, 0, H16>(a, acc, mw, nw, lane);
-    } else {
-#define EPI_CASE(BF, E, NS)                                                                      \
+      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
+  } else if constexpr (SCORES) {  // seg/det proj -> map partials
+    if (key == AACLIP_EPI_LEAKY)
+      wave_epilogue<RM, RN, 3, AACLIP_EPI_LEAKY, 0, H16>(a, acc, mw, nw, lane);
+    else
+      wave_epilogue<RM, RN, 3, 0, 0, H16>(a, acc, mw, nw, lane);
+  } else {
+#define EPI_CASE(BF, E)                                                                          \
   if (bf16_out == (BF) && key == (E)) {                                                          \
-    if constexpr (PERSIST)                                                                       \
-      wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane);                        \
-    else                                                                                         \
-      wave_epilogue_lds<RM, RN, BF ? 1 : 0, E, H16>(a, acc, mw, nw, lane,                        \
-                                                    ((E) & AACLIP_EPI_BIAS) ? lbp : nullptr, slot); \
-    s_prev = full && !(a.dbg & 2) ? (NS) : 0;                                                    \
+    wave_epilogue_lds<RM, RN, BF ? 1 : 0, E, H16>(a, acc, mw, nw, lane,                          \
+                                                  ((E) & AACLIP_EPI_BIAS) ? lbp : nullptr, slot); \
   } else
-      EPI_CASE(true, AACLIP_EPI_BIAS, RM * RN / 2)
-      EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU, RM * RN / 2)
-      EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU, RM * RN / 2)
-      EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID, RM * RN)
-      EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16, RM * RN + RM * RN / 2)
-      EPI_CASE(false, AACLIP_EPI_LEAKY, RM * RN)
+    EPI_CASE(true, AACLIP_EPI_BIAS)
+    EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)
+    EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)
+    EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)
+    EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)
+    EPI_CASE(false, AACLIP_EPI_LEAKY)
 #undef EPI_CASE
-      // any other flag combination (row remap, 16-bit rows + residual, ...): run-time flags
-      if constexpr (PERSIST) {
-        if (bf16_out)
-          wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane);
-        else
-          wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane);
-      } else {
-        if (bf16_out)
-          wave_epilogue_lds<RM, RN, 1, -1, H16>(a, acc, mw, nw, lane, lds_bias ? lbp : nullptr, slot);
-        else
-          wave_epilogue_lds<RM, RN, 0, -1, H16>(a, acc, mw, nw, lane, lds_bias ? lbp : nullptr, slot);
-      }
-    }
-    if (!PERSIST || !has_next) break;
-    if (wr == 1) __builtin_amdgcn_s_barrier();
-    tile += gridDim.x;
-    tm = tm_n;
-    tn = tn_n;
-    a_vo = a_vo_next;
-    w_vo = w_vo_next;
+    // any other flag combination (row remap, 16-bit rows + residual, ...): run-time flags
+    if (bf16_out)
+      wave_epilogue_lds<RM, RN, 1, -1, H16>(a, acc, mw, nw, lane, lds_bias ? lbp : nullptr, slot);
+    else
+      wave_epilogue_lds<RM, RN, 0, -1, H16>(a, acc, mw, nw, lane, lds_bias ? lbp : nullptr, slot);
   }
 #undef PH_SYNC_MFMA
   if (stamp) ts[2] = __builtin_amdgcn_s_memtime();
@@ -1230,132 +1170,6 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
     wave_epilogue<RM, RN, 0, -1, 2>(a, acc, mw, nw, lane);
 }
 
-// ======================= two-workgroups-per-CU bf16 kernel (256x128 tile, K-step 32)
-// The 8-phase kernel fills a CU with ONE workgroup (8 waves x 224+ VGPRs, 128 KiB LDS):
-// while its waves run the epilogue (bias / GELU / residual, then the stores) the CU's
-// matrix cores idle -- measured 2.3 ms of the 13.9 ms two-stream C2 step
-// (tools/epi_bound.py). This kernel keeps the same 128x64 wave tile (so the same
-// wave_epilogue) in 4-wave workgroups of 72 KiB LDS and <= 256 VGPRs: two workgroups
-// share each CU, one wave of each per SIMD, and one's epilogue runs beside the other's
-// main loop. K-step 32 (64-B LDS rows) so a 3-stage ring fits the 80 KiB share; the
-// ring's end-of-step wait is COUNTED (the next stage's 6 DMA pieces per wave stay in
-// flight across the barrier). LDS image: lane (fr, fq) reads 16-B chunk fq of row r,
-// stored at physical chunk fq ^ ((r >> 2) & 2) -- conflict-free for ds_read_b128's
-// lane groups (searched exhaustively); the swizzle is applied on the DMA source side.
-// Same K order as every other 16-bit family (K ascending, one fp32 accumulator per
-// output), so the results are bit-identical to them.
-template <bool H16>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_pp2_kernel(GemmArgs a) {
-  using V8 = h16x8_t<H16>;
-  constexpr int BM = 256, BN = 128, TM = 128, TN = 64, RM = 8, RN = 4;
-  constexpr int A_BYTES = BM * 64, STAGE = (BM + BN) * 64;  // 16 KiB + 8 KiB
-  constexpr int NS = 3;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int t = threadIdx.x;
-  const int lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-  int tm, tn;
-  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
-  const int m0 = tm * BM, n0 = tn * BN;
-  const auto ars = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)((uint32_t)a.M * (uint32_t)a.lda * 2u),
-                                                     0x00020000);
-  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, (int)((uint32_t)a.N * (uint32_t)a.ldw * 2u),
-                                                     0x00020000);
-  // DMA piece = 16 rows x 64 B; lane -> row lane/4 of the piece, physical chunk lane%4,
-  // logical (source) chunk (lane%4) ^ ((row >> 2) & 2). Wave w fills A pieces w, w+4, w+8,
-  // w+12 and B pieces w, w+4. Rows past M / N read as zeros (buffer range check).
-  const int prow = lane >> 2;
-  const int lchunk = ((lane & 3) ^ ((prow >> 2) & 2)) * 8;  // elements
-  int a_vo[4], b_vo[2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) a_vo[i] = ((m0 + (i * 4 + wid) * 16 + prow) * (int)a.lda + lchunk) * 2;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) b_vo[i] = ((n0 + (i * 4 + wid) * 16 + prow) * (int)a.ldw + lchunk) * 2;
-  auto stage = [&](int kt, int buf) {
-    char* dst = smem + buf * STAGE;
-    const int ko = kt * 64;  // bytes
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, LDS_PTR(dst + (i * 4 + wid) * 1024), 16, a_vo[i], ko, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + A_BYTES + (i * 4 + wid) * 1024), 16, b_vo[i], ko,
-                                               0, 0);
-  };
-  const int sw = (fq ^ ((fr >> 2) & 2)) << 4;
-  const int a_rd = (wr * TM + fr) * 64 + sw, b_rd = A_BYTES + (wc * TN + fr) * 64 + sw;
-  float4_t acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-  const int nk = a.K / 32;
-  stage(0, 0);
-  if (nk > 1) stage(1, 1);
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // stage kt landed; kt+1 may fly
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of stage kt landed, stage kt-1 read
-    if (kt + 2 < nk) stage(kt + 2, cur == 0 ? 2 : cur - 1);
-    const char* st = smem + cur * STAGE;
-    V8 bf[RN];
-#pragma unroll
-    for (int j = 0; j < RN; ++j) bf[j] = *(const V8*)(st + b_rd + j * 1024);
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const V8 af = *(const V8*)(st + a_rd + i * 1024);
-#pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = mfma16(bf[j], af, acc[i][j]);
-    }
-    cur = cur == NS - 1 ? 0 : cur + 1;
-  }
-  const int mw = m0 + wr * TM, nw = n0 + wc * TN;
-  if (a.dbg & 1) {
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-  const bool bf16_out = a.out_dtype != AACLIP_F32;
-  const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
-#define EPI_CASE(BF, E)                                                   \
-  if (bf16_out == (BF) && key == (E)) {                                   \
-    wave_epilogue<RM, RN, BF ? 1 : 0, E, 0, H16>(a, acc, mw, nw, lane);   \
-    return;                                                               \
-  }
-  EPI_CASE(true, AACLIP_EPI_BIAS)
-  EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_GELU)
-  EPI_CASE(true, AACLIP_EPI_BIAS | AACLIP_EPI_QGELU)
-  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID)
-  EPI_CASE(false, AACLIP_EPI_BIAS | AACLIP_EPI_RESID | AACLIP_EPI_AUX_BF16)
-  EPI_CASE(false, AACLIP_EPI_BIAS)
-  EPI_CASE(false, AACLIP_EPI_LEAKY)
-#undef EPI_CASE
-  if (bf16_out)
-    wave_epilogue<RM, RN, 1, -1, 0, H16>(a, acc, mw, nw, lane);
-  else
-    wave_epilogue<RM, RN, 0, -1, 0, H16>(a, acc, mw, nw, lane);
-}
-
-template <bool H16>
-int launch_bf16_pp2(GemmArgs a, hipStream_t s) {
-  if (a.N % 128 || a.K % 32) return AACLIP_ERR_ARG;
-  a.tiles_m = ceil_div(a.M, 256);
-  a.tiles_n = a.N / 128;
-  const size_t lds = 3 * (256 + 128) * 64;
-  static unsigned attr_dev = 0;
-  if (!lds_attr_once((const void*)gemm_bf16_pp2_kernel<H16>, (int)lds, attr_dev)) return AACLIP_ERR_LAUNCH;
-  gemm_bf16_pp2_kernel<H16><<<a.tiles_m * a.tiles_n, 256, lds, s>>>(a);
-  AACLIP_CHECK_LAUNCH();
-  return AACLIP_OK;
-}
-
 int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
@@ -1369,21 +1183,16 @@ int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
 
 int cu_count();
 
-template <bool H16, bool PERSIST = false, bool SCORES = false>
+template <bool H16, bool SCORES = false>
 int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   if (a.N % 256 || a.K % 64) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
-  const int tiles = a.tiles_m * a.tiles_n;
-  // persistent: one workgroup per CU, a multiple of 8 so each keeps its XCD's tile run;
-  // the K-step stream across tiles needs an even K-step count (stage = kt & 1)
-  const int cus = cu_count() & ~7;
-  if (PERSIST && !((a.K / 64) % 2 == 0 && tiles > cus && cus > 0)) return launch_bf16_8ph<H16, false>(a, s);
   const size_t lds = 2 * 4 * 128 * 128 + 1024;  // the ring + the tile's bias
   static unsigned attr_dev = 0;
-  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, PERSIST, SCORES>, (int)lds, attr_dev))
+  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, SCORES>, (int)lds, attr_dev))
     return AACLIP_ERR_LAUNCH;
-  gemm_bf16_8ph_kernel<H16, PERSIST, SCORES><<<PERSIST ? cus : tiles, 512, lds, s>>>(a);
+  gemm_bf16_8ph_kernel<H16, SCORES><<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -1475,8 +1284,7 @@ int pinned_family(int dtype, int M, int N, int K) {
 // launch (captured graphs keep it); thread-local, so it needs no global pin state.
 thread_local int t_concurrent = 0;
 
-enum Kern { KERN_256x256 = 1, KERN_256x128 = 2, KERN_8PH = 3, KERN_8PH_PERSIST = 5, KERN_320x256 = 8,
-            KERN_128x128 = 9, KERN_PP2 = 10, KERN_64x64 = 11 };
+enum Kern { KERN_256x256 = 1, KERN_256x128 = 2, KERN_8PH = 3, KERN_320x256 = 8, KERN_128x128 = 9, KERN_64x64 = 11 };
 
 // The kernel a 16-bit GEMM of this shape launches: the A/B variant hook, else a pin,
 // else the concurrent-chunk rule, else the per-shape heuristic (fewer tile rounds
@@ -1496,15 +1304,9 @@ int choose16(int dtype, int M, int N, int K, bool fits) {
     case 4:  // 8-phase for the wide GEMMs only (N >= 2048), 320x256 below
       if (N % 256 == 0 && (fam == 3 || N >= 2048) && fits) return KERN_8PH;
       break;
-    case 5:  // A/B: the persistent 8-phase kernel wherever N % 256 == 0
-      if (N % 256 == 0 && fits) return KERN_8PH_PERSIST;
-      break;
     case 9: return KERN_128x128;  // 128x128 everywhere (A/B)
     case 11:  // 64x64 everywhere (A/B)
       if (N % 64 == 0) return KERN_64x64;
-      break;
-    case 10:  // two workgroups per CU, 256x128 tile, K-step 32
-      if (fits && K % 32 == 0) return KERN_PP2;
       break;
     case 8:  // A/B: the 320x256 LDS-DMA kernel wherever N % 256 == 0 (the pre-heuristic default)
       if (N % 256 == 0) return KERN_320x256;
@@ -1528,11 +1330,9 @@ int dispatch16(GemmArgs a, hipStream_t s) {
   switch (choose16(H16 ? AACLIP_F16 : AACLIP_BF16, M, N, a.K, fits)) {
     case KERN_256x256: return launch_bf16<256, 256, 2, 4, 0, H16>(a, s);
     case KERN_8PH: return launch_bf16_8ph<H16>(a, s);
-    case KERN_8PH_PERSIST: return launch_bf16_8ph<H16, true>(a, s);
     case KERN_320x256: return launch_bf16<320, 256, 2, 4, 0, H16>(a, s);
     case KERN_128x128: return launch_bf16<128, 128, 2, 2, 0, H16>(a, s);
     case KERN_64x64: return launch_bf16<64, 64, 2, 2, 0, H16>(a, s);
-    case KERN_PP2: return launch_bf16_pp2<H16>(a, s);
     default: return launch_bf16<256, 128, 4, 2, 0, H16>(a, s);
   }
 }
@@ -1548,11 +1348,9 @@ extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
   switch (choose16(in_dtype, M, N, K, fits)) {
     case KERN_256x256: return "gemm_bf16_kernel<256,256,2,4>";
     case KERN_8PH: return "gemm_bf16_8ph_kernel<256,256>";
-    case KERN_8PH_PERSIST: return "gemm_bf16_8ph_kernel<256,256,persistent>";
     case KERN_320x256: return "gemm_bf16_kernel<320,256,2,4>";
     case KERN_128x128: return "gemm_bf16_kernel<128,128,2,2>";
     case KERN_64x64: return "gemm_bf16_kernel<64,64,2,2>";
-    case KERN_PP2: return "gemm_bf16_pp2_kernel<256,128>";
     default: return "gemm_bf16_kernel<256,128,4,2>";
   }
 }
@@ -1560,8 +1358,8 @@ extern "C" const char* aaclip_gemm_plan(int in_dtype, int M, int N, int K) {
 extern "C" int aaclip_gemm_pin(int in_dtype, int M, int N, int K, int family) {
   AACLIP_REQUIRE((in_dtype == AACLIP_BF16 || in_dtype == AACLIP_F16) && M > 0 && N > 0 && K > 0);
   AACLIP_REQUIRE(family == 0 || family == 1 || family == 2 || family == 3 || family == 8 || family == 9 ||
-                 family == 10 || family == 11);
-  AACLIP_REQUIRE(family == 0 || family == 2 || family == 10 || family == 11 || N % 256 == 0);
+                 family == 11);
+  AACLIP_REQUIRE(family == 0 || family == 2 || family == 11 || N % 256 == 0);
   std::lock_guard<std::mutex> lk(g_pin_mu);
   const int n = g_npins.load(std::memory_order_relaxed);
   for (int i = 0; i < n; ++i)
@@ -1590,13 +1388,13 @@ extern "C" int aaclip_gemm_concurrent(int on, int* previous) {
 
 extern "C" int aaclip_set_gemm_variant(int variant) {
   // bits 0-3: tile family (0 default = per-shape choice, 1 = 256x256, 2 = 256x128, 3/4 = 256x256
-  // 8-phase ping-pong everywhere / for N >= 2048, 5 = persistent 8-phase, 6 = MX fp8 on the
-  // 256x256 LDS-DMA kernel instead
-  // of its 8-phase default, 8 = 320x256 everywhere, 9 = 128x128, 10 = two-workgroup 256x128,
-  // 11 = 64x64); bits 4-7: tile-order
+  // 8-phase ping-pong everywhere / for N >= 2048, 6 = MX fp8 on the 256x256 LDS-DMA kernel
+  // instead of its 8-phase default, 8 = 320x256 everywhere, 9 = 128x128, 11 = 64x64; the
+  // persistent 8-phase family 5 and the two-workgroup family 10 measured slower and were
+  // removed in round 5); bits 4-7: tile-order
   // group height (0 = 4); bit 8: setprio around the MFMA cluster; bits 9-11: diagnostics
   const int fam = variant & 15, grp = (variant >> 4) & 15;
-  if (variant < 0 || variant >= 4096 || fam > 11 || fam == 7) return AACLIP_ERR_ARG;
+  if (variant < 0 || variant >= 4096 || fam > 11 || fam == 5 || fam == 7 || fam == 10) return AACLIP_ERR_ARG;
   g_gemm_variant = fam;
   g_group_m = grp ? grp : 4;
   g_setprio = (variant >> 8) & 1;
@@ -1656,8 +1454,7 @@ extern "C" int aaclip_gemm_scores(int in_dtype, int M, int N, int K, const void*
   hipStream_t s = (hipStream_t)stream;
   const bool h16 = in_dtype == AACLIP_F16;
   const bool fits = (int64_t)M * lda * 2 < (1ll << 31) && (int64_t)N * ldw * 2 < (1ll << 31);
-  // the same per-shape choice as aaclip_gemm (same K order, same bits); the A/B-only
-  // families without this epilogue (persistent 8-phase, two-workgroup) take the 8-phase one
+  // the same per-shape choice as aaclip_gemm (same K order, same bits)
   switch (choose16(in_dtype, M, N, K, fits)) {
     case KERN_256x256:
       return h16 ? launch_bf16<256, 256, 2, 4, 0, true>(a, s) : launch_bf16<256, 256, 2, 4, 0, false>(a, s);
@@ -1671,7 +1468,7 @@ extern "C" int aaclip_gemm_scores(int in_dtype, int M, int N, int K, const void*
       return h16 ? launch_bf16<256, 128, 4, 2, 0, true>(a, s) : launch_bf16<256, 128, 4, 2, 0, false>(a, s);
     default:
       if (!fits) return h16 ? launch_bf16<320, 256, 2, 4, 0, true>(a, s) : launch_bf16<320, 256, 2, 4, 0, false>(a, s);
-      return h16 ? launch_bf16_8ph<true, false, true>(a, s) : launch_bf16_8ph<false, false, true>(a, s);
+      return h16 ? launch_bf16_8ph<true, true>(a, s) : launch_bf16_8ph<false, true>(a, s);
   }
 }
 

@@ -229,27 +229,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int out_dtype, const flo
     store_any<VEC>((char*)y + (size_t)row * ldy * esize(out_dtype), out_dtype, o, lane);
 }
 
-// x += d (deferred residual: d = out-proj's acc + bias), then y = LN(x); the add is the
-// GEMM epilogue's (acc + bias) + x with the operands swapped -- fp32 addition commutes.
-template <int VEC>
-__global__ __launch_bounds__(256) void residual_ln_kernel(int out_dtype, float* x, const float* d, const float* w,
-                                                          const float* b, void* y, int rows, uint8_t* sc,
-                                                          int64_t ld_sc) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  constexpr int D = 256 * VEC;
-  float* xr = x + (size_t)row * D;
-  float4_t v[VEC], a[VEC], o[VEC];
-  load_f32<VEC>(xr, v, lane);
-  load_f32<VEC>(d + (size_t)row * D, a, lane);
-#pragma unroll
-  for (int c = 0; c < VEC; ++c) v[c] += a[c];
-  store_any<VEC>(xr, AACLIP_F32, v, lane);
-  layer_norm<VEC>(v, w, b, o, lane);
-  store_out<VEC>(y, out_dtype, row, sc, ld_sc, o, lane);
-}
-
 template <int VEC>
 __global__ __launch_bounds__(256) void text_embed_ln_kernel(int out_dtype, const int32_t* tokens,
                                                             const float* temb, const float* pos,
@@ -580,16 +559,6 @@ extern "C" int aaclip_layernorm(int out_dtype, const float* x, int64_t ldx, cons
   if (rows == 0) return AACLIP_OK;
   DISPATCH_VEC(width, layernorm_kernel<V><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
                           out_dtype, x, ldx, w, b, y, ldy, rows, (uint8_t*)y_mx, ld_mx));
-  AACLIP_CHECK_LAUNCH();
-  return AACLIP_OK;
-}
-
-extern "C" int aaclip_residual_layernorm(int out_dtype, float* x, const float* d, const float* w, const float* b,
-                                         void* y, int rows, int width, void* y_mx, int64_t ld_mx, void* stream) {
-  AACLIP_REQUIRE(mx_ok(out_dtype, y_mx, ld_mx, rows, width) && x && d && w && b && y && rows >= 0);
-  if (rows == 0) return AACLIP_OK;
-  DISPATCH_VEC(width, residual_ln_kernel<V><<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(
-                          out_dtype, x, d, w, b, y, rows, (uint8_t*)y_mx, ld_mx));
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }

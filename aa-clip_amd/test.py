@@ -5,6 +5,7 @@ same flow, same outputs), running AdaptedCLIP on the MI355X kernels.
     python test.py --dataset synthetic --allow_random_init --img_size 336  (C1: no files needed)
     python test.py --dataset synthetic_mvtec --allow_random_init --img_size 336  (C4's 15-class flow)
     torchrun --nproc-per-node 8 test.py ...   (C3-style: each class's images sharded over 8 GPUs)
+    AACLIP_REHEARSAL=1 torchrun --nproc-per-node 2 test.py ...   (the same ranks, all on cuda:0 over gloo)
 
 Differences from the reference, all on the host side:
   * the per-batch loop calls the fused AdaptedCLIP.predict (map + score in one
@@ -153,6 +154,8 @@ def parse_args(argv=None):
     parser.add_argument("--gpu_preprocess", action=argparse.BooleanOptionalAction, default=True,
                         help="real datasets: decode on the host, resize + normalise on the GPU (bit-exact with the "
                              "Pillow path; the default); --no-gpu_preprocess = the Pillow transform in the workers")
+    parser.add_argument("--results_json", type=str, default="",
+                        help="also write the final table (rank 0) to this JSON file")
     return parser.parse_args(argv)
 
 
@@ -170,10 +173,17 @@ def run(args):
         raise RuntimeError("the AA-CLIP MI355X build needs a GPU (no CPU path)")
     if world > 1:  # one process per GPU (torchrun); image-sharded classes
         import torch.distributed as dist
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # AACLIP_REHEARSAL=1: every rank on cuda:0 over gloo -- the multi-rank harness (shards,
+        # gathers onto rank 0, rank-0 metrics) on a one-GPU box, where RCCL refuses two ranks
+        # on one device (bench.py's AACLIP_BENCH_REHEARSAL is the same switch)
+        rehearsal = os.environ.get("AACLIP_REHEARSAL") == "1"
+        local = 0 if rehearsal else int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         if not dist.is_initialized():
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if rehearsal:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         device = torch.device("cuda", local)
     else:
         device = torch.device("cuda:0")
@@ -265,6 +275,11 @@ def run(args):
         df.loc[len(df) - 1, "class name"] = "Average"
         logger.info("final results:\n%s", df.to_string(index=False, justify="center"))
         print(df.to_string(index=False, justify="center"))
+        if args.results_json:  # the table as JSON (tests compare sharded and single-process runs)
+            import json
+            with open(args.results_json, "w") as f:
+                json.dump({"world": world, "rows": df.astype({c: float for c in df.columns[1:]}).to_dict("records")},
+                          f)
     return df, ctx
 
 

@@ -150,8 +150,7 @@ int aaclip_quant_fp8_rows(int in_dtype, const void* x, int64_t ldx, void* q, int
  * 320x256 LDS-DMA, whichever needs fewer tile rounds weighted by per-tile cost,
  * and 128x128 when that choice would fill under half the CUs; else 256x128),
  * 1 = 256x256 (N % 256 == 0), 2 = 256x128, 3 = 8-phase everywhere, 4 = 8-phase
- * for N >= 2048 only, 8 = 320x256 everywhere, 9 = 128x128 everywhere, 10 = two
- * 4-wave 256x128 workgroups per CU (K-step 32; N % 128 == 0, K % 32 == 0), 11 = 64x64
+ * for N >= 2048 only, 8 = 320x256 everywhere, 9 = 128x128 everywhere, 11 = 64x64
  * everywhere (N % 64 == 0; the default for single-image shapes); for the
  * fp8 MX GEMM: 0 = 8-phase ping-pong (default), 6 = the 256x256 LDS-DMA kernel; bits 4-7:
  * tile-order group height (0 = 4); bit 8: s_setprio around the MFMA cluster;
@@ -167,7 +166,7 @@ int aaclip_set_gemm_variant(int variant);
 /*
  * Pin the tile family aaclip_gemm uses for one (in_dtype, M, N, K) (bf16 / f16):
  * 1 = 256x256, 2 = 256x128, 3 = 256x256 8-phase ping-pong, 8 = 320x256,
- * 9 = 128x128, 10 = two 4-wave 256x128 workgroups per CU, 11 = 64x64, 0 = unpin (back to the
+ * 9 = 128x128, 11 = 64x64, 0 = unpin (back to the
  * heuristic). Set by a measuring tuner at
  * engine setup (aaclip/ops.py tune_gemm); every family accumulates K in the same
  * order, so a pin changes speed, never bits. Process-global (mutex-guarded), host
@@ -216,8 +215,7 @@ int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
 
 /* Tuning hook for the 16-bit attention kernel: 0 = default (3), 1 = 4 waves x 32 queries per
  * workgroup, 2 = 2 waves x 64 queries, 3 = 1 with each full key tile phase-split so one
- * query block's softmax runs beside the other's MFMAs, 4 = 3 with the exponentials formed
- * ahead of the deferred-max check (same bits). Process-global; for benchmarking. */
+ * query block's softmax runs beside the other's MFMAs. Process-global; for benchmarking. */
 int aaclip_set_attn_variant(int variant);
 
 /*
@@ -258,18 +256,6 @@ int aaclip_block_tail(int out_dtype, float* x, const float* u, float adapt_weigh
 int aaclip_layernorm(int out_dtype, const float* x, int64_t ldx, const float* w,
                      const float* b, void* y, int64_t ldy, int rows, int width,
                      void* y_mx, int64_t ld_mx, void* stream);
-
-/*
- * Deferred residual add + LN: x[row] = x[row] + d[row] (fp32, in place); y = LN(x).
- * With d = the out-proj GEMM's (acc + bias) written without a residual read, this is
- * the same fp32 add the GEMM epilogue's AACLIP_EPI_RESID performs (the add commutes),
- * so x and y are bit-identical to out-proj(+resid) followed by aaclip_layernorm.
- * x, d: [rows, width] fp32 contiguous; y as aaclip_layernorm (ldy = width).
- * Replaces: the residual add of transformer.py:256 + ln_2 of transformer.py:257.
- */
-int aaclip_residual_layernorm(int out_dtype, float* x, const float* d, const float* w,
-                              const float* b, void* y, int rows, int width, void* y_mx,
-                              int64_t ld_mx, void* stream);
 
 /*
  * (embed_ln, block_tail, layernorm) out_dtype AACLIP_FP8: the LayerNorm row (h / y)
@@ -350,22 +336,6 @@ int aaclip_anomaly_map(int in_dtype, const void* const* levels, int n_levels, in
                        void* stream);
 
 /*
- * aaclip_anomaly_map (normalised features) in ONE launch: one workgroup per (image,
- * grid row) streams that row's patch positions through every level into grid_ws
- * (>= batch*g*g fp32), then counts itself into the output bands (kBand = 8 output
- * rows) whose blur + bilinear source rows include its row; the workgroup that
- * completes a band computes it. Same bits as aaclip_anomaly_map. band_counters:
- * batch * ceil(out_size / 8) int32, ZERO before the first call; every call leaves them
- * zero (one counter set per concurrently running call). out_size <= 1024, g <= 64.
- * Measured 115-119 us in the C2 step vs 61 us for aaclip_anomaly_map (B = 32): the
- * engine keeps the two-launch form; this entry is opt-in (AACLIP_MAP_FUSED=1).
- * Replaces: test.py:86-93 + forward_utils.py:196-213.
- */
-int aaclip_anomaly_map_fused(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
-                             const float* T, int batch, int g, int channels, int out_size, int ksize,
-                             float sigma, float* grid_ws, int* band_counters, float* out, void* stream);
-
-/*
  * The predict path's map + image score from aaclip_gemm_scores partials (the level
  * projections are never written as rows): part [batch*g*g][ld_part] fp32 holds, per
  * patch row, n_levels levels (+ the det projection when with_det) of 24 float4
@@ -391,22 +361,6 @@ int aaclip_anomaly_map_partials(const float* part, int64_t ld_part, int n_levels
 int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld, const float* T,
                        int batch, int n_patch, int channels, int normalize, float* partial,
                        float* det, float* score, void* stream);
-
-/*
- * The test path's whole per-batch tail in one pass over the projections: the
- * level-summed anomaly map (as aaclip_anomaly_map, normalised features) AND the
- * image score (as aaclip_image_score; same bits for both). Stage 1 reads every
- * patch row of all n_levels levels and of det_raw (levels[l] and det_raw share the
- * row stride ld, e.g. the engine's one [rows, (L+1)*768] projection buffer) once,
- * writing the score grid and the det partials; then blur + upsample and the det
- * finalisation. grid_ws >= batch*g*g fp32, partial as for aaclip_image_score;
- * det (optional) [batch, 768], score [batch], out [batch, S, S].
- * Replaces: test.py:80-93 after the forward + forward_utils.py:196-213.
- */
-int aaclip_anomaly_map_score(int in_dtype, const void* const* levels, int n_levels, int64_t ld,
-                             const void* det_raw, const float* T, int batch, int g, int channels,
-                             int out_size, int ksize, float sigma, float* grid_ws, float* partial,
-                             float* out, float* det, float* score, void* stream);
 
 /*
  * Device metrics_eval for one class (replaces forward_utils.py:233-280 + the

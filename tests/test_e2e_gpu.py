@@ -349,25 +349,3 @@ def test_quick_gelu_towers_parity(dev, weights, dtype):
         enc = TextEngine(tp, ad, dtype=dtype, quick_gelu=True).encode(torch.from_numpy(q["tok_abnormal"]).to(dev))
         ref = q[f"enc_abnormal_{key}"]
         np.testing.assert_allclose(enc.cpu().numpy(), ref, atol=tol * max(1.0, np.abs(ref).max()), rtol=tol * 10)
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32, torch.float8_e4m3fn])
-def test_deferred_residual_bit_identical(dev, weights, dtype):
-    """out-proj written as acc + bias with the residual add done by ln_2
-    (aaclip_residual_layernorm) gives the same bits as the out-proj epilogue's fp32
-    read-modify-write: the same add, operands swapped (reference transformer.py:256-257).
-    fp8 = config C5's default scope (bf16 out-proj, MX ln_2 output)."""
-    eng = _visual(weights, dtype)
-    g = torch.Generator(device=dev).manual_seed(8)
-    x = torch.randn(3, 3, 336, 336, device=dev, generator=g)
-    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
-    out = []
-    for defer in (False, True):
-        eng.defer_resid = defer
-        eng._ws.clear()
-        seg, det = eng.forward(x)
-        m, s = eng.predict(x, T, "Industrial", streams=2)
-        out.append(([t.clone() for t in seg], det.clone(), m.clone(), s.clone()))
-    (s0, d0, m0, c0), (s1, d1, m1, c1) = out
-    assert all(torch.equal(a, b) for a, b in zip(s0, s1))
-    assert torch.equal(d0, d1) and torch.equal(m0, m1) and torch.equal(c0, c1)

@@ -22,12 +22,12 @@ H16 = torch.float16
 
 
 # ----------------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 8, 9, 10])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8, 9, 11])
 @pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768, 1024), (18464, 4096, 1024)])
 def test_gemm_f16_variants(dev, variant, M, N, K):
     """Every 16-bit tile family (default per-shape choice, 256x256, 256x128, 8-phase,
     320x256, 128x128) on fp16 operands, fp32 out, float64 reference."""
-    if variant in (1, 3, 5, 8) and N % 256:
+    if variant in (1, 3, 8) and N % 256:
         pytest.skip("256-wide tile needs N % 256 == 0")
     torch.manual_seed(M * 5 + N)
     a = torch.randn(M, K, device=dev).to(H16)
@@ -43,7 +43,7 @@ def test_gemm_f16_variants(dev, variant, M, N, K):
     assert (out.double() - ref).abs().max().item() < 1e-4 * ref.abs().max().item() + 1e-5
 
 
-@pytest.mark.parametrize("variant", [0, 3, 5, 8, 9, 10])
+@pytest.mark.parametrize("variant", [0, 3, 8, 9, 11])
 def test_gemm_f16_epilogues(dev, variant):
     """fp16 output (bias, bias + GELU), fp32 residual in place + fp16 aux copy, LeakyReLU."""
     torch.manual_seed(11)

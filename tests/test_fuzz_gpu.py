@@ -13,7 +13,7 @@ from aaclip import _lib, ops
 
 pytestmark = pytest.mark.gpu
 
-FAMILIES = (0, 1, 2, 3, 5, 8, 9, 11)  # default dispatch + every forced tile family
+FAMILIES = (0, 1, 2, 3, 8, 9, 11)  # default dispatch + every forced tile family
 
 
 def _gemm_case(seed):
@@ -92,7 +92,7 @@ def test_attention_fuzz(dev, seed):
     H = int(rng.choice([1, 2, 12, 16]))
     causal = bool(rng.random() < 0.3)
     dt = torch.float32 if seed % 4 == 1 else (torch.float16 if seed % 3 == 0 else torch.bfloat16)
-    variant = int(rng.choice([0, 1, 2, 3, 4]))
+    variant = int(rng.choice([0, 1, 2, 3]))
     g = torch.Generator(device=dev).manual_seed(seed)
     qkv = (torch.randn(B * N, 3 * H * 64, device=dev, generator=g) * 1.5).to(dt)
     out = torch.empty(B * N, H * 64, device=dev, dtype=dt)

@@ -42,3 +42,39 @@ def test_bench_two_ranks_real_engine(dev):
     assert d["gather_verified"] and d["own_slice_verified"], d
     assert d["checked_shard"]["rank"] == 1 and d["checked_shard"]["images"] == [32, 64]
     assert line["step_outputs_verified"]["finite"] and line["step_outputs_verified"]["equal_to_one_stream_eager"]
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(900)
+def test_harness_two_ranks_real_engine(dev, tmp_path):
+    """The harness's multi-rank path (aa-clip_amd/test.py under torchrun: each class's images
+    sharded by shard_range, per-rank predict on the real engine, maps / scores / masks /
+    labels / names gathered onto rank 0, rank-0 device metrics_eval) against the same harness
+    in one process. 7 images per class over 2 ranks (an uneven 4 + 3 shard), 15 classes
+    (C4's synthetic_mvtec flow). Both runs are FRESH child processes; the rehearsal puts
+    both ranks on cuda:0 over gloo (AACLIP_REHEARSAL=1). Reference: test.py:53-99,211-249."""
+    script = os.path.join(ROOT, "aa-clip_amd", "test.py")
+    common = ["--dataset", "synthetic_mvtec", "--allow_random_init", "--synthetic_n", "7", "--img_size", "336",
+              "--compute_dtype", "fp16"]
+    one, two = tmp_path / "single.json", tmp_path / "two_ranks.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-u", script, *common, "--save_path", str(tmp_path / "s1"),
+                        "--results_json", str(one)], cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    env2 = dict(env, AACLIP_REHEARSAL="1")
+    r = subprocess.run([sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script, *common,
+                        "--save_path", str(tmp_path / "s2"), "--results_json", str(two)],
+                       cwd=ROOT, env=env2, capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    a, b = json.loads(one.read_text()), json.loads(two.read_text())
+    assert a["world"] == 1 and b["world"] == 2
+    assert len(a["rows"]) == 16  # 15 classes + the average row
+    print(b["rows"][-1])
+    assert a["rows"] == b["rows"]  # every per-class pixel / image AUROC and AP, exactly

@@ -3,7 +3,7 @@ ONE process and timed in interleaved rounds (the same-box, same-clock A/B the st
 numbers need). An arm is `name=attr:value,attr:value` (value parsed as int, else kept as
 a string), set on the engine before its graph is captured; every arm's map and score are
 compared bit for bit with arm 0's.
-usage: python tools/engine_ab.py base= defer=defer_resid:1 [--streams 1] [--dtype fp16]"""
+usage: python tools/engine_ab.py base= rows=map_partials:0 [--streams 1] [--dtype fp16]"""
 import argparse
 import os
 import sys
