@@ -104,6 +104,7 @@ __global__ __launch_bounds__(256) void patch_scores_kernel(LevelPtrs lv, int nl,
                                                            int64_t ld, const float* T, int rows,
                                                            int normalize, int mode, int group,
                                                            float* out) {
+  AACLIP_TRACE_SCOPE(TR_PATCH_SCORES);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -333,6 +334,7 @@ template <int C, int K>
 __global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, float* out, int g, int S,
                                                            int ksize_rt, Gauss gw, int softmax, float scale,
                                                            int xrows, int brows) {
+  AACLIP_TRACE_SCOPE(TR_BLUR);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   blur_band<C, K>(grid, out, blockIdx.y, blockIdx.x, g, S, ksize_rt, gw, softmax, scale, xrows, brows, smem,
                   threadIdx.x);
@@ -357,6 +359,7 @@ __global__ __launch_bounds__(256) void partial_scores_kernel(const float* __rest
                                                              int with_det, int rows, float* __restrict__ grid,
                                                              float* __restrict__ det_rows) {
 #pragma clang fp contract(off)
+  AACLIP_TRACE_SCOPE(TR_PARTIAL_SCORES);
   const int lane = threadIdx.x & 31;
   const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
   if (row >= rows) return;
@@ -392,6 +395,7 @@ __global__ __launch_bounds__(64) void blur_upsample_score_kernel(const float* gr
                                                                  int brows, const float* det_rows, int n_patch,
                                                                  float* score) {
 #pragma clang fp contract(off)
+  AACLIP_TRACE_SCOPE(TR_BLUR_SCORE);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if (blockIdx.x == 0 && det_rows) {
     const float* d = det_rows + (size_t)blockIdx.y * n_patch;
@@ -414,6 +418,7 @@ constexpr int kDetRows = 16;
 template <bool F32IN>
 __global__ __launch_bounds__(64 * kDetRows) void map_det_kernel(int64_t ld, const void* det, int n_patch,
                                                                 int normalize, float* partial, int nchunk) {
+  AACLIP_TRACE_SCOPE(TR_DET);
   __shared__ float red[kDetRows][768];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int b = blockIdx.y, ch = blockIdx.x;
@@ -465,6 +470,7 @@ __global__ __launch_bounds__(64 * kDetRows) void map_det_kernel(int64_t ld, cons
 __global__ __launch_bounds__(768) void det_finalize_kernel(const float* partial, int nchunk,
                                                            int n_patch, const float* T,
                                                            float* det, float* score) {
+  AACLIP_TRACE_SCOPE(TR_DET);
   __shared__ float red[12];
   const int b = blockIdx.x, j = threadIdx.x;
   const float* pp = partial + (size_t)b * nchunk * 768 + j;
@@ -682,3 +688,5 @@ extern "C" int aaclip_image_score(int in_dtype, const void* det_raw, int64_t ld,
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
+
+AACLIP_TRACE_SETTER(trace_set_anomaly_map)

@@ -307,6 +307,7 @@ template <bool H16, int QB, int NW, int NS, int SPLIT>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_kernel(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int batch, int N, int H, int flags,
     uint8_t* __restrict__ out_mx, int64_t ld_mx) {
+  AACLIP_TRACE_SCOPE(TR_ATTN);
   const int causal = flags & AACLIP_ATTN_CAUSAL;
   constexpr int QW = 16 * QB;     // queries per wave
   constexpr int QT = QW * NW;     // queries per workgroup
@@ -595,6 +596,7 @@ constexpr int F32_LDK = 68;
 
 __global__ __launch_bounds__(256, 2) void attn_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                           int N, int H, int causal) {
+  AACLIP_TRACE_SCOPE(TR_ATTN_F32);
   constexpr int QB = 2;  // 16-query blocks per wave
   __shared__ __attribute__((aligned(16))) float Ks[KT][F32_LDK];
   __shared__ __attribute__((aligned(16))) float Vs[KT][F32_LDK];
@@ -795,3 +797,5 @@ extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
+
+AACLIP_TRACE_SETTER(trace_set_attention)

@@ -108,3 +108,60 @@ inline bool lds_attr_once(const void* fn, int bytes, unsigned& done) {
 }
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- step timeline (diagnostic)
+// Built only with -DAACLIP_TRACE (`make trace` -> libaaclip_hip_trace.so; the product
+// library compiles none of this): every wave of an instrumented kernel appends one
+// record {t0, t1 (s_memrealtime, the chip-wide 100 MHz clock), tag, HW_ID, XCC_ID,
+// workgroup} to a caller-provided device buffer (aaclip_trace_buffer), so a tool can
+// rebuild which CU ran what when over a whole concurrent step (tools/timeline.py).
+// Records go to a per-CU slab (slot = XCC, SE, SH, CU: 2048 slots) through a per-slot
+// counter 64 B apart: one counter for the whole chip serialised ~1.7 M same-address
+// atomics per step and doubled the step time. Written with vector stores after the
+// wave's own last memory op.
+enum TraceTag : uint32_t {
+  TR_GEMM_8PH = 1, TR_GEMM_TILE = 2, TR_GEMM_FP8MX = 3, TR_ATTN = 4, TR_LAYERNORM = 5, TR_BLOCK_TAIL = 6,
+  TR_EMBED_LN = 7, TR_IM2COL = 8, TR_PARTIAL_SCORES = 9, TR_BLUR_SCORE = 10, TR_GEMM_F32 = 11, TR_ATTN_F32 = 12,
+  TR_PATCH_SCORES = 13, TR_BLUR = 14, TR_DET = 15
+};
+constexpr int kTraceSlots = 2048;  // XCC (3 bits) x SE (3) x SH (1) x CU (4)
+#ifdef AACLIP_TRACE
+struct TraceState {
+  uint32_t* rec;   // [kTraceSlots][cap][8] uint32
+  uint32_t* count; // [kTraceSlots][16] uint32 (slot counters, one per 64 B)
+  uint32_t cap;    // records per slot
+};
+static __device__ TraceState g_trace;
+struct TraceScope {
+  uint64_t t0;
+  uint32_t tag;
+  __device__ __forceinline__ explicit TraceScope(uint32_t tag_) : tag(tag_) { t0 = __builtin_amdgcn_s_memrealtime(); }
+  __device__ __forceinline__ ~TraceScope() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if ((threadIdx.x & 63) == 0 && g_trace.rec) {
+      const uint32_t slot = ((xcc & 7) << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15);
+      const uint32_t i = atomicAdd(g_trace.count + slot * 16, 1u);
+      if (i < g_trace.cap) {
+        const uint32_t wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        uint4* r = (uint4*)(g_trace.rec + ((size_t)slot * g_trace.cap + i) * 8);
+        r[0] = uint4{(uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32)};
+        r[1] = uint4{tag, hw, xcc, wg};
+      }
+    }
+  }
+};
+#define AACLIP_TRACE_SCOPE(tag) TraceScope _aaclip_trace_scope(tag)
+// one per translation unit: points this TU's g_trace at the buffer (host side)
+#define AACLIP_TRACE_SETTER(name)                                                          \
+  int name(void* rec, void* count, unsigned cap) {                                        \
+    TraceState t{(uint32_t*)rec, (uint32_t*)count, cap};                                  \
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &t, sizeof t) == hipSuccess ? 0 : -1;  \
+  }
+#else
+#define AACLIP_TRACE_SCOPE(tag) ((void)0)
+#define AACLIP_TRACE_SETTER(name)
+#endif

@@ -152,6 +152,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(int out_dtype, float* x, 
                                                        const float* pb, const float* w1,
                                                        const float* b1, void* h, int rows,
                                                        int n_tok, uint8_t* sc, int64_t ld_sc) {
+  AACLIP_TRACE_SCOPE(TR_EMBED_LN);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(256) void block_tail_kernel(int out_dtype, float* x
                                                          const float* pw, const float* pb,
                                                          void* tap, int rows, int n_tok, uint8_t* sc,
                                                          int64_t ld_sc) {
+  AACLIP_TRACE_SCOPE(TR_BLOCK_TAIL);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -217,6 +219,7 @@ template <int VEC>
 __global__ __launch_bounds__(256) void layernorm_kernel(int out_dtype, const float* x, int64_t ldx,
                                                         const float* w, const float* b, void* y,
                                                         int64_t ldy, int rows, uint8_t* sc, int64_t ld_sc) {
+  AACLIP_TRACE_SCOPE(TR_LAYERNORM);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -334,6 +337,7 @@ __global__ __launch_bounds__(256) void anchor_reduce_kernel(const float* emb, in
 // thread). Pure copy + the same conversions: the same bits as im2col_kernel.
 __global__ __launch_bounds__(256) void im2col_band_kernel(int out_dtype, const float* img, void* cols, int C,
                                                           int S, int P, int g, int kp) {
+  AACLIP_TRACE_SCOPE(TR_IM2COL);
   extern __shared__ __attribute__((aligned(16))) float band[];  // [P][S]
   const int c = blockIdx.x % C;
   const int bp = blockIdx.x / C;
@@ -646,3 +650,5 @@ extern "C" int aaclip_quant_fp8_mx(int in_dtype, const void* x, int64_t ldx, voi
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
+
+AACLIP_TRACE_SETTER(trace_set_rows)

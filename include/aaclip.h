@@ -50,9 +50,23 @@ extern "C" {
                                   exclusive with AACLIP_EPI_GELU               */
 
 /* ABI version (bumped on any signature change; 2 = MX fp8 LayerNorm outputs, 3 = fp16 dtype,
- * aaclip_patch_logits, any-size blur_upsample) and the target. */
+ * aaclip_patch_logits, any-size blur_upsample; 6 = round 5: the rejected A/B entry points
+ * removed, aaclip_trace_buffer added) and the target. */
 int aaclip_abi_version(void);
 const char* aaclip_arch(void);
+
+/*
+ * Diagnostic step timeline (trace builds only: `make trace` -> libaaclip_hip_trace.so;
+ * the product library returns AACLIP_ERR_ARG). Every wave of an instrumented kernel
+ * appends one record of 8 uint32 {t0 lo, t0 hi, t1 lo, t1 hi, tag, HW_ID, XCC_ID,
+ * workgroup} to the slab of its CU: slot = XCC << 8 | SE << 5 | SH << 4 | CU (2048
+ * slots), records [2048][capacity][8], counter [2048][16] uint32 (slot s counts at
+ * counter[16 s]; zero it before a traced run); a slot's records past capacity are
+ * dropped (its counter still counts them). t0 / t1 are s_memrealtime (100 MHz,
+ * chip-wide). records = counter = NULL, capacity = 0 turns it off. Not a reference
+ * interface: tools/timeline.py reads it to measure the gap share of a step.
+ */
+int aaclip_trace_buffer(void* records, void* counter, unsigned capacity);
 
 /*
  * C[M,N] = epilogue(A[M,K] . W[N,K]^T)        (nn.Linear / conv-as-GEMM)

@@ -1,0 +1,228 @@
+"""Step timeline of the C2 step from inside the kernels: which CU ran what, when.
+
+Loads the trace build of the library (`make -C aa-clip_amd/csrc trace` ->
+libaaclip_hip_trace.so; every wave of an instrumented kernel appends {t0, t1, tag, HW_ID,
+XCC_ID, workgroup} with t from s_memrealtime, the chip-wide 100 MHz clock), replays the
+captured C2 step (B = 32, two streams, bf16, the bench's graph) and reports, per replay:
+
+  * step window (first wave start .. last wave end) and the replay's HIP-event time;
+  * CU busy fraction = sum over CUs of the union of their waves' intervals / (CUs x window):
+    1 - that is the share of the step in which a CU holds no wave at all (launch ramps,
+    partial last tile rounds, dependent-launch gaps) -- the "gap share";
+  * SIMD busy fraction (the same per SIMD: a CU whose one GEMM workgroup uses all four
+    SIMDs counts busy on each);
+  * per op: wave-time, CU-time (union per CU of that op's waves) and the CU-time share;
+  * the CU-busy count over time (binned), and per-CU idle gaps by length.
+
+usage (GPU box): python tools/timeline.py [--replays 3] [--streams 2] [--out gpurun_out/timeline.json]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TRACE_LIB = os.path.join(ROOT, "aa-clip_amd", "aaclip", "libaaclip_hip_trace.so")
+os.environ.setdefault("AACLIP_LIB", TRACE_LIB)
+sys.path[:0] = [ROOT, os.path.join(ROOT, "aa-clip_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from aaclip import _lib  # noqa: E402
+from aaclip.engine import VisualEngine  # noqa: E402
+
+KIND = {1: "gemm_8ph", 2: "gemm_tile", 3: "gemm_fp8mx", 4: "attention", 5: "layernorm", 6: "block_tail",
+        7: "embed_ln", 8: "im2col", 9: "map_partials", 10: "map_blur_score", 11: "gemm_f32", 12: "attn_f32",
+        13: "patch_scores", 14: "blur", 15: "det"}
+EPI_BIAS, EPI_GELU, EPI_LEAKY, EPI_RESID = 1, 2, 4, 8
+
+
+def op_of(tag: int) -> str:
+    kid = tag & 15
+    kind = KIND.get(kid, f"k{kid}")
+    if kid not in (1, 2, 3, 11):
+        return kind
+    n, k, epi = ((tag >> 4) & 255) * 64, ((tag >> 12) & 255) * 64, tag >> 20
+    if n == 3072 and k == 1024:
+        return "qkv"
+    if n == 4096 and k == 1024:
+        return "c_fc"
+    if n == 1024 and k == 4096:
+        return "c_proj"
+    if n == 1024 and k == 1024:
+        return "adapter" if epi & EPI_LEAKY else "out_proj"
+    if k == 640:
+        return "patch_embed"
+    if n in (768, 1536):
+        return "level_proj"
+    return f"gemm N{n} K{k}"
+
+
+def segments(gid: np.ndarray, s: np.ndarray, e: np.ndarray):
+    """Merge the intervals [s, e) of every group gid into disjoint busy segments.
+    Returns (segment group, segment start, segment end), sorted by group then start."""
+    o = np.lexsort((s, gid))
+    g, s, e = gid[o], s[o], e[o]
+    big = float(e.max() + 1.0)
+    ce = np.maximum.accumulate(e + g * big) - g * big  # running max of the end inside each group
+    new = np.ones(len(s), bool)
+    new[1:] = (g[1:] != g[:-1]) | (s[1:] > ce[:-1])
+    starts = np.flatnonzero(new)
+    ends = np.append(starts[1:], len(s)) - 1
+    return g[starts], s[starts], ce[ends]
+
+
+def analyse(rec: np.ndarray, event_ms: float, bin_us: float = 2.0) -> dict:
+    t0 = rec[:, 0].astype(np.int64) | (rec[:, 1].astype(np.int64) << 32)
+    t1 = rec[:, 2].astype(np.int64) | (rec[:, 3].astype(np.int64) << 32)
+    tag, hw, xcc = rec[:, 4], rec[:, 5], rec[:, 6]
+    lo = t0.min()
+    s = (t0 - lo) / 100.0  # us (100 MHz)
+    e = (t1 - lo) / 100.0
+    window = float(e.max())
+    simd = ((hw >> 4) & 3).astype(np.int64)
+    cu = ((hw >> 8) & 15).astype(np.int64)
+    sh = ((hw >> 12) & 1).astype(np.int64)
+    se = ((hw >> 13) & 7).astype(np.int64)
+    cu_key = ((xcc & 15).astype(np.int64) << 8) | (se << 5) | (sh << 4) | cu
+    simd_key = (cu_key << 2) | simd
+    utags, tinv = np.unique(tag, return_inverse=True)
+    names = sorted({op_of(int(t)) for t in utags})
+    op_id = np.array([names.index(op_of(int(t))) for t in utags])[tinv]
+    n_cu = len(np.unique(cu_key))
+    n_simd = len(np.unique(simd_key))
+    sg, ss, se_ = segments(cu_key, s, e)
+    cu_busy = float((se_ - ss).sum())
+    _, s2, e2 = segments(simd_key, s, e)
+    simd_busy = float((e2 - s2).sum())
+    per_op = {}
+    og, os_, oe = segments(op_id * 4096 + cu_key, s, e)
+    for i, o in enumerate(names):
+        m = op_id == i
+        cu_time = float((oe - os_)[og // 4096 == i].sum())
+        per_op[o] = {"waves": int(m.sum()), "wave_time_ms": round(float((e[m] - s[m]).sum()) / 1e3, 3),
+                     "cu_time_ms": round(cu_time / 1e3, 3), "cu_time_share": round(cu_time / (n_cu * window), 4)}
+    # idle gaps per CU: before the first segment, between segments, after the last one
+    first = np.ones(len(sg), bool)
+    first[1:] = sg[1:] != sg[:-1]
+    last = np.ones(len(sg), bool)
+    last[:-1] = sg[1:] != sg[:-1]
+    prev_end = np.concatenate([[0.0], se_[:-1]])
+    gap = np.where(first, ss, ss - prev_end)
+    tail = window - se_[last]
+    g = np.concatenate([gap, tail])
+    buckets = {"<2us": float(g[g < 2].sum()), "2-10us": float(g[(g >= 2) & (g < 10)].sum()),
+               "10-50us": float(g[(g >= 10) & (g < 50)].sum()), ">=50us": float(g[g >= 50].sum())}
+    # busy CUs over time: coverage of the merged CU segments per bin
+    nb = int(np.ceil(window / bin_us))
+    edges = np.arange(nb + 1) * bin_us
+    occ = np.zeros(nb)
+    for a, b in zip(ss, se_):
+        i0, i1 = int(a // bin_us), min(nb - 1, int(b // bin_us))
+        if i0 == i1:
+            occ[i0] += (b - a) / bin_us
+        else:
+            occ[i0] += (edges[i0 + 1] - a) / bin_us
+            occ[i0 + 1:i1] += 1.0
+            occ[i1] += (b - edges[i1]) / bin_us
+    return {
+        "records": int(len(rec)), "cus": n_cu, "simds": n_simd,
+        "window_ms": round(window / 1e3, 3), "event_ms": round(event_ms, 3),
+        "cu_busy_frac": round(cu_busy / (n_cu * window), 4),
+        "gap_share": round(1 - cu_busy / (n_cu * window), 4),
+        "simd_busy_frac": round(simd_busy / (n_simd * window), 4),
+        "cu_idle_ms_by_gap_length": {k: round(v / n_cu / 1e3, 4) for k, v in buckets.items()},
+        "busy_cus_over_time": {"bin_us": bin_us, "mean": round(float(occ.mean()), 1),
+                               "frac_time_under_half": round(float((occ < n_cu / 2).mean()), 4),
+                               "frac_time_under_90pct": round(float((occ < 0.9 * n_cu).mean()), 4),
+                               "bins": [round(float(v), 1) for v in occ]},
+        "per_op": per_op,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--replays", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--img-size", type=int, default=336)
+    ap.add_argument("--dtype", choices=("bf16", "fp16"), default="bf16")
+    ap.add_argument("--cap", type=int, default=16384, help="records per CU slot (2048 slots)")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "timeline.json"))
+    ap.add_argument("--raw", default="", help="also save the last replay's records (npz: t0, t1 in 10 ns ticks "
+                                               "from the first start, tag, cu slot, simd)")
+    a = ap.parse_args()
+    from bench import synthetic_visual_weights
+    dev = torch.device("cuda:0")
+    B, S = a.batch, a.img_size
+    vp, ad = synthetic_visual_weights(dev, n_tok=(S // 14) ** 2 + 1)
+    eng = VisualEngine(vp, ad, dtype=torch.bfloat16 if a.dtype == "bf16" else torch.float16)
+    g = torch.Generator(device=dev).manual_seed(111)
+    x = torch.randn(B, 3, S, S, device=dev, generator=g)
+    T = torch.nn.functional.normalize(torch.randn(768, 2, device=dev, generator=g), dim=0).contiguous()
+    run = eng.graphed_predict(B, S, "Industrial", streams=a.streams)
+    slots = 2048  # XCC x SE x SH x CU, common.h kTraceSlots
+    recs = torch.zeros(slots, a.cap, 8, device=dev, dtype=torch.int32)
+    cnt = torch.zeros(slots, 16, device=dev, dtype=torch.int32)
+    st = torch.cuda.current_stream()
+
+    def timed(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(n):
+            run(x, T)
+        e1.record(st)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    for _ in range(5):
+        run(x, T)
+    torch.cuda.synchronize()
+    base_ms = timed(20)  # untraced (records pointer NULL: the trace build's kernels skip the store)
+    out = {"config": {"batch": B, "img_size": S, "streams": a.streams, "dtype": a.dtype, "graph": True},
+           "untraced_step_ms": round(base_ms, 3), "replays": []}
+    _lib.call("aaclip_trace_buffer", recs.data_ptr(), cnt.data_ptr(), a.cap)
+    try:
+        for r in range(a.replays):
+            cnt.zero_()
+            torch.cuda.synchronize()
+            ms = timed(1)
+            n = cnt[:, 0].cpu()
+            if int(n.max()) > a.cap:
+                raise RuntimeError(f"trace slot too small: {int(n.max())} records > {a.cap}")
+            used = torch.nonzero(n).flatten()
+            rr = recs.cpu()
+            rec = torch.cat([rr[int(i), :int(n[i])] for i in used]).numpy().view(np.uint32)
+            t = time.time()
+            res = analyse(rec, ms)
+            res["max_records_per_cu"] = int(n.max())
+            if a.raw and r == a.replays - 1:
+                t0 = rec[:, 0].astype(np.int64) | (rec[:, 1].astype(np.int64) << 32)
+                t1 = rec[:, 2].astype(np.int64) | (rec[:, 3].astype(np.int64) << 32)
+                lo = t0.min()
+                hw, xcc = rec[:, 5], rec[:, 6]
+                slot = ((xcc & 7) << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
+                np.savez_compressed(a.raw, t0=(t0 - lo).astype(np.uint32), t1=(t1 - lo).astype(np.uint32),
+                                    tag=rec[:, 4], slot=slot.astype(np.uint16), simd=((hw >> 4) & 3).astype(np.uint8),
+                                    wg=rec[:, 7])
+            res["analysis_s"] = round(time.time() - t, 1)
+            if r:
+                res["busy_cus_over_time"].pop("bins")  # one replay's curve is enough
+            out["replays"].append(res)
+            print(json.dumps({k: v for k, v in res.items() if k not in ("busy_cus_over_time", "per_op")}), flush=True)
+    finally:
+        _lib.call("aaclip_trace_buffer", None, None, 0)
+    traced_ms = timed(20)
+    out["traced_step_ms_after"] = round(traced_ms, 3)
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    r0 = out["replays"][-1]
+    print(json.dumps({"untraced_step_ms": out["untraced_step_ms"], "gap_share": r0["gap_share"],
+                      "simd_busy_frac": r0["simd_busy_frac"],
+                      "per_op": {k: v["cu_time_share"] for k, v in r0["per_op"].items()}}))
+
+
+if __name__ == "__main__":
+    main()
