@@ -576,8 +576,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
     }
     if (q < N) {
       uint16_t* o = out + ((size_t)b * N + q) * HDt + h * HD_ + 16 * (g & 1) + 8 * (g >> 1);
-      st16<AACLIP_WT_ATTN>(o, w[0]);
-      st16<AACLIP_WT_ATTN>(o + 32, w[1]);
+      *(uint4*)(o) = w[0];
+      *(uint4*)(o + 32) = w[1];
     }
   }
 }

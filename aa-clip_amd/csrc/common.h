@@ -109,47 +109,6 @@ inline bool lds_attr_once(const void* fn, int bytes, unsigned& done) {
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
-// ---------------------------------------------------------------- store cache policy
-// 16-B / 8-B global stores, plain or write-through (sc1: written through to memory and
-// DROPPED from the XCD's L2, where a plain store keeps the line dirty in L2 --
-// MI355X_MICROARCH 'stores of each flavour'). Build-time switches per kernel family for
-// A/B builds: AACLIP_WT_GEMM, AACLIP_WT_ATTN, AACLIP_WT_ROWS.
-// GEMM epilogues store write-through by default (round 5): a GEMM's output is consumed by
-// the next op's tiles on all 8 XCDs, so keeping it dirty in the producing XCD's 4-MiB L2
-// only displaces the A / W panels the running tiles re-read; C2 step 2366 -> 2620
-// images/s (+10.7 %, same box, 2 interleaved rounds, same bits: profiles/r05/
-// store_policy_ab.txt). Attention and row-kernel outputs written through measured
-// neutral to -0.6 % and stay plain.
-#ifndef AACLIP_WT_GEMM
-#define AACLIP_WT_GEMM 1
-#endif
-#ifndef AACLIP_WT_ATTN
-#define AACLIP_WT_ATTN 0
-#endif
-#ifndef AACLIP_WT_ROWS
-#define AACLIP_WT_ROWS 0
-#endif
-typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
-typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
-template <bool WT>
-__device__ __forceinline__ void st16(void* p, uint4 v) {
-  if constexpr (WT)
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(__builtin_bit_cast(u32x4_t, v)) : "memory");
-  else
-    *(uint4*)p = v;
-}
-template <bool WT>
-__device__ __forceinline__ void st16(void* p, float4_t v) {
-  st16<WT>(p, __builtin_bit_cast(uint4, v));
-}
-template <bool WT>
-__device__ __forceinline__ void st8(void* p, uint2 v) {
-  if constexpr (WT)
-    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(__builtin_bit_cast(u32x2_t, v)) : "memory");
-  else
-    *(uint2*)p = v;
-}
-
 // ---------------------------------------------------------------- step timeline (diagnostic)
 // Built only with -DAACLIP_TRACE (`make trace` -> libaaclip_hip_trace.so; the product
 // library compiles none of this): every wave of an instrumented kernel appends one

@@ -322,7 +322,7 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
         pr[q] = float4_t{sum_over_fq(ss), sum_over_fq(x0), sum_over_fq(x1), 0.f};
       }
       if (m < a.M && fq < RN / 2)
-        st16<AACLIP_WT_GEMM>((float*)a.C + orow * a.ldc + (nw >> 3) + 4 * fq, (fq == 0) ? pr[0] : pr[RN / 2 - 1]);
+        *(float4_t*)((float*)a.C + orow * a.ldc + (nw >> 3) + 4 * fq) = (fq == 0) ? pr[0] : pr[RN / 2 - 1];
       continue;
     }
     if constexpr (OUTM == 2) {
@@ -341,7 +341,7 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
       }
       transpose_fq(d);
       if (m < a.M) {
-        st16<AACLIP_WT_GEMM>((uint8_t*)a.C + orow * a.ldc + nw + 16 * fq, uint4{d[0], d[1], d[2], d[3]});
+        *(uint4*)((uint8_t*)a.C + orow * a.ldc + nw + 16 * fq) = uint4{d[0], d[1], d[2], d[3]};
         const int blk = nw >> 6;
         if (fq == 0) a.c_mx[((size_t)(blk >> 1) * a.ld_cmx + orow) * 2 + (blk & 1)] = (uint8_t)(e + 127);
       }
@@ -355,14 +355,14 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
     if (m < a.M) {
       if constexpr (BF16OUT) {
 #pragma unroll
-        for (int q = 0; q < RN / 2; ++q) st16<AACLIP_WT_GEMM>((uint16_t*)a.C + orow * a.ldc + pcol + 32 * q, pk[q]);
+        for (int q = 0; q < RN / 2; ++q) *(uint4*)((uint16_t*)a.C + orow * a.ldc + pcol + 32 * q) = pk[q];
       } else {
 #pragma unroll
-        for (int j = 0; j < RN; ++j) st16<AACLIP_WT_GEMM>((float*)a.C + orow * a.ldc + ncol + 16 * j, v[j]);
+        for (int j = 0; j < RN; ++j) *(float4_t*)((float*)a.C + orow * a.ldc + ncol + 16 * j) = v[j];
       }
       if (epi & AACLIP_EPI_AUX_BF16) {
 #pragma unroll
-        for (int q = 0; q < RN / 2; ++q) st16<AACLIP_WT_GEMM>((uint16_t*)a.aux + orow * a.ldaux + pcol + 32 * q, pk[q]);
+        for (int q = 0; q < RN / 2; ++q) *(uint4*)((uint16_t*)a.aux + orow * a.ldaux + pcol + 32 * q) = pk[q];
       }
     }
   }
@@ -388,7 +388,6 @@ __device__ __forceinline__ void wave_epilogue(const GemmArgs& a, float4_t (&acc)
 template <int RM, int RN, int OUTM, int EPI, bool H16, int SCALED = 0, int PD = 2>
 __device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&acc)[RM][RN], int mw, int nw,
                                                   int lane, const float* lbias, char* slot) {
-  constexpr bool SC1 = AACLIP_WT_GEMM;  // write-through output stores (common.h)
   static_assert(RN == 4 && OUTM >= 0 && OUTM <= 2, "one wave's 64 columns: fp32, 16-bit or fp8 MX rows");
   static_assert(SCALED == 0 || SCALED == 2, "no per-row A scales");
   static_assert(PD >= 2 && PD <= RM, "residual ring depth");
@@ -468,7 +467,7 @@ __device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&
         asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
         continue;
       }
-      if (m < a.M) st16<SC1>((uint8_t*)a.C + orow * a.ldc + nw + 16 * qc, w);
+      if (m < a.M) *(uint4*)((uint8_t*)a.C + orow * a.ldc + nw + 16 * qc) = w;
       const int mr = mw + 16 * i + fr;  // the block scale: one byte per row, lanes fq = 0
       if (mr < a.M && fq == 0) {
         const int blk = nw >> 6;
@@ -492,7 +491,7 @@ __device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&
       }
       if (m < a.M) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) st16<SC1>((uint16_t*)a.C + orow * a.ldc + nw + 8 * qc + 32 * k, w[k]);
+        for (int k = 0; k < 2; ++k) *(uint4*)((uint16_t*)a.C + orow * a.ldc + nw + 8 * qc + 32 * k) = w[k];
       }
     } else {
 #pragma unroll
@@ -511,16 +510,16 @@ __device__ __forceinline__ void wave_epilogue_lds(const GemmArgs& a, float4_t (&
       if (m < a.M && BF16OUT) {  // 16-bit rows with a residual: 8 B per lane
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          st8<SC1>((uint16_t*)a.C + orow * a.ldc + nw + 4 * qc + 16 * k,
-                   uint2{pack_h16x2<H16>(u[k][0], u[k][1]), pack_h16x2<H16>(u[k][2], u[k][3])});
+          *(uint2*)((uint16_t*)a.C + orow * a.ldc + nw + 4 * qc + 16 * k) =
+              uint2{pack_h16x2<H16>(u[k][0], u[k][1]), pack_h16x2<H16>(u[k][2], u[k][3])};
       } else if (m < a.M) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) st16<SC1>((float*)a.C + orow * a.ldc + nw + 4 * qc + 16 * k, u[k]);
+        for (int k = 0; k < 4; ++k) *(float4_t*)((float*)a.C + orow * a.ldc + nw + 4 * qc + 16 * k) = u[k];
         if (epi & AACLIP_EPI_AUX_BF16) {
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            st8<SC1>((uint16_t*)a.aux + orow * a.ldaux + nw + 4 * qc + 16 * k,
-                     uint2{pack_h16x2<H16>(u[k][0], u[k][1]), pack_h16x2<H16>(u[k][2], u[k][3])});
+            *(uint2*)((uint16_t*)a.aux + orow * a.ldaux + nw + 4 * qc + 16 * k) =
+                uint2{pack_h16x2<H16>(u[k][0], u[k][1]), pack_h16x2<H16>(u[k][2], u[k][3])};
         }
       }
     }
@@ -1404,7 +1403,7 @@ extern "C" int aaclip_set_gemm_variant(int variant) {
   g_group_m = grp ? grp : 4;
   g_setprio = (variant >> 8) & 1;
   // bit 9 skip epilogue, bit 10 skip the global stores, bit 11 the 8-phase kernel's
-  // per-wave s_memtime stamps into the aux pointer (bf16 / fp32 epilogues without aux only),
+  // per-wave s_memtime stamps into the aux pointer (bf16 / fp32 epilogues without aux only)
   g_dbg = (variant >> 9) & 7;
   return AACLIP_OK;
 }

@@ -49,7 +49,7 @@ template <int VEC>
 __device__ __forceinline__ void store_any(void* p, int dtype, const float4_t (&v)[VEC], int lane) {
   if (dtype == AACLIP_F32) {
 #pragma unroll
-    for (int c = 0; c < VEC; ++c) st16<AACLIP_WT_ROWS>((float*)p + 256 * c + 4 * lane, v[c]);
+    for (int c = 0; c < VEC; ++c) *(float4_t*)((float*)p + 256 * c + 4 * lane) = v[c];
   } else {
     const bool h = dtype == AACLIP_F16;
     uint16_t* q = (uint16_t*)p;
@@ -58,7 +58,7 @@ __device__ __forceinline__ void store_any(void* p, int dtype, const float4_t (&v
       uint2 r;
       r.x = h ? pack_f16x2(v[c][0], v[c][1]) : pack_bf16x2(v[c][0], v[c][1]);
       r.y = h ? pack_f16x2(v[c][2], v[c][3]) : pack_bf16x2(v[c][2], v[c][3]);
-      st8<AACLIP_WT_ROWS>(q + 256 * c + 4 * lane, r);
+      *(uint2*)(q + 256 * c + 4 * lane) = r;
     }
   }
 }
