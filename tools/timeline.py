@@ -34,15 +34,14 @@ from aaclip.engine import VisualEngine  # noqa: E402
 
 KIND = {1: "gemm_8ph", 2: "gemm_tile", 3: "gemm_fp8mx", 4: "attention", 5: "layernorm", 6: "block_tail",
         7: "embed_ln", 8: "im2col", 9: "map_partials", 10: "map_blur_score", 11: "gemm_f32", 12: "attn_f32",
-        13: "patch_scores", 14: "blur", 15: "det"}
+        13: "patch_scores", 14: "blur", 15: "det", 16: "map_fused"}
 EPI_BIAS, EPI_GELU, EPI_LEAKY, EPI_RESID = 1, 2, 4, 8
 
 
 def op_of(tag: int) -> str:
     kid = tag & 15
-    kind = KIND.get(kid, f"k{kid}")
-    if kid not in (1, 2, 3, 11):
-        return kind
+    if kid not in (1, 2, 3, 11):  # GEMM tags carry N, K and the epilogue above bit 4
+        return KIND.get(tag, f"k{tag}")
     n, k, epi = ((tag >> 4) & 255) * 64, ((tag >> 12) & 255) * 64, tag >> 20
     if n == 3072 and k == 1024:
         return "qkv"
