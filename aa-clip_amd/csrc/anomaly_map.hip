@@ -341,17 +341,29 @@ __global__ __launch_bounds__(64) void blur_upsample_kernel(const float* grid, fl
 }
 
 // Stage 1 from GEMM partials (aaclip_gemm_scores wrote, per patch row and 32-column group
-// g of each level, {||v||^2, v.t0, v.t1}): one HALF-wave per patch row, lane q < 24 holds
-// group q of every level (one float4 per level), fixed-order butterfly sums over the 32
-// lanes (every lane ends with the same bits), then patch_row_score's normalise + anchor
-// arithmetic (normalize = 1). The det level (with_det) leaves d.t1 / ||d|| per row for
-// the image score. 1.9 KB read per C2 patch row instead of 15 KB of projected rows.
+// q of each level, {||v||^2, v.t0, v.t1}): 8 lanes per patch row, 8 rows per wave. Lane j
+// loads groups j, j+8, j+16 of every level (three float4 per level: each load instruction
+// covers 128 contiguous bytes of 8 rows) and sums them, (g_j + g_j+8) + g_j+16; the 8 lane
+// sums meet in three DPP butterfly steps inside the 8-lane group (quad swaps 1 and 2, then
+// the half-row mirror i <-> 7 - i), a + b on one lane and b + a on its partner, so every lane
+// ends with the same bits. Then patch_row_score's normalise + anchor arithmetic
+// (normalize = 1). The det level (with_det) leaves d.t1 / ||d|| per row for the image
+// score. 1.9 KB read per C2 patch row instead of 15 KB of projected rows. (Round 4 used one
+// half-wave per row and five-step shuffle sums: 24 of 32 lanes loading, 75 LDS swizzles per
+// 2 rows; 18.4 us at B = 32 in the bench's rocprofv3 trace.)
 constexpr int kGroups = 768 / 32;  // 32-column groups per level
+constexpr int kRowLanes = 8;       // lanes per patch row in partial_scores_kernel
 
-__device__ __forceinline__ float half_sum(float v) {
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
-  return v;
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  const float o = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
+                                                                           true));
+  return v + o;
+}
+__device__ __forceinline__ float sum8(float v) {
+  v = dpp_add<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v = dpp_add<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  return dpp_add<0x141>(v);  // row_half_mirror
 }
 
 template <int NLMAX>
@@ -360,30 +372,34 @@ __global__ __launch_bounds__(256) void partial_scores_kernel(const float* __rest
                                                              float* __restrict__ det_rows) {
 #pragma clang fp contract(off)
   AACLIP_TRACE_SCOPE(TR_PARTIAL_SCORES);
-  const int lane = threadIdx.x & 31;
-  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
-  if (row >= rows) return;
-  const float* pr = part + (size_t)row * ld + 4 * lane;
+  const int j = threadIdx.x & (kRowLanes - 1);
+  const int row = blockIdx.x * (256 / kRowLanes) + (threadIdx.x / kRowLanes);
+  if (row >= rows) return;  // all 8 lanes of a row leave together: the DPP steps stay inside a row's lanes
+  const float* pr = part + (size_t)row * ld + 4 * j;
   const int nt = nl + with_det;
-  float4_t v[NLMAX + 1];
+  float4_t v[NLMAX + 1][3];
 #pragma unroll
   for (int l = 0; l <= NLMAX; ++l)
-    if (l < nt) v[l] = lane < kGroups ? *(const float4_t*)(pr + l * 4 * kGroups) : float4_t{0.f, 0.f, 0.f, 0.f};
+    if (l < nt) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) v[l][k] = *(const float4_t*)(pr + l * 4 * kGroups + 4 * kRowLanes * k);
+    }
   float acc = 0.f;
 #pragma unroll
   for (int l = 0; l <= NLMAX; ++l) {
     if (l < nt) {
-      const float ss = half_sum(v[l][0]), a0 = half_sum(v[l][1]), a1 = half_sum(v[l][2]);
+      const float4_t t = (v[l][0] + v[l][1]) + v[l][2];
+      const float ss = sum8(t[0]), a0 = sum8(t[1]), a1 = sum8(t[2]);
       const float inv = 1.0f / fmaxf(sqrtf(ss), 1e-12f);
       if (l < nl) {
         const float A0 = 100.0f * (a0 * inv), A1 = 100.0f * (a1 * inv);
         acc += (A1 + 1.0f - A0) / 2.0f;
-      } else if (lane == 0) {
+      } else if (j == 0) {
         det_rows[row] = a1 * inv;  // normalize(d) . t1
       }
     }
   }
-  if (lane == 0) grid[row] = acc;
+  if (j == 0) grid[row] = acc;
 }
 
 // Stage 2 + the image score: blur_upsample_kernel's bands, and the band-0 wave of each
@@ -643,10 +659,10 @@ extern "C" int aaclip_anomaly_map_partials(const float* part, int64_t ld_part, i
   const int rows = batch * g * g;
   hipStream_t s = (hipStream_t)stream;
   if (n_levels <= 4)
-    partial_scores_kernel<4><<<ceil_div(rows, 8), 256, 0, s>>>(part, ld_part, n_levels, with_det, rows, grid_ws,
+    partial_scores_kernel<4><<<ceil_div(rows, 256 / kRowLanes), 256, 0, s>>>(part, ld_part, n_levels, with_det, rows, grid_ws,
                                                                 det_ws);
   else
-    partial_scores_kernel<kMaxLevels><<<ceil_div(rows, 8), 256, 0, s>>>(part, ld_part, n_levels, with_det, rows,
+    partial_scores_kernel<kMaxLevels><<<ceil_div(rows, 256 / kRowLanes), 256, 0, s>>>(part, ld_part, n_levels, with_det, rows,
                                                                          grid_ws, det_ws);
   AACLIP_CHECK_LAUNCH();
   const Gauss gw = ksize > 0 ? gaussian_weights(ksize, sigma) : Gauss{};

@@ -54,11 +54,18 @@ def main():
         t_bu = graph_time(lambda: ops.blur_upsample(ws[:B * P].view(B, 1, g, g), m.view(B, 1, S, S), ksize=7, sigma=1.0))
         t_u0 = graph_time(lambda: ops.blur_upsample(ws[:B * P].view(B, 1, g, g), m.view(B, 1, S, S), ksize=0, sigma=0.0))
         t_all = graph_time(lambda: ops.anomaly_map(lv, T, m, ws, g=g, ksize=7, sigma=1.0))
+        # predict()'s form: the map + image score from per-(row, 32-column) GEMM partials
+        part = torch.rand(B * P, (L + 1) * 4 * ops.SCORE_GROUPS, device=dev) + 0.5
+        dws, sc = torch.empty(B * P, device=dev), torch.empty(B, device=dev)
+        t_pm = graph_time(lambda: ops.anomaly_map_partials(part, L, m, ws, g=g, ksize=7, sigma=1.0, det_ws=dws, score=sc))
+        survey = B * 3.99e6 if S == 336 else None  # SURVEY 8(d) bytes per image at 336 px
         rd = L * B * P * 768 * 4
         wr = B * S * S * 4
         out[S] = {"patch_scores_us": round(t_ps, 2), "patch_scores_TBs": round(rd / t_ps / 1e6, 2),
                   "blur_upsample_us": round(t_bu, 2), "upsample_only_us": round(t_u0, 2), "blur_upsample_TBs": round(wr / t_bu / 1e6, 2),
-                  "anomaly_map_us": round(t_all, 2), "anomaly_map_TBs": round((rd + wr) / t_all / 1e6, 2)}
+                  "anomaly_map_us": round(t_all, 2), "anomaly_map_TBs": round((rd + wr) / t_all / 1e6, 2),
+                  "partials_map_score_us": round(t_pm, 2),
+                  "partials_frac_vs_survey_bytes": round(survey / t_pm / 1e6 / 8.0, 3) if survey else None}
     print(json.dumps(out))
 
 
