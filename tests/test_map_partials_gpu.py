@@ -100,3 +100,45 @@ def test_partials_args_rejected_before_launch(dev):
                   ops._ptr(grid), None, ops._ptr(out), None, ops._stream())
     torch.cuda.synchronize()
     assert (grid == 7.0).all() and (out == 7.0).all()
+
+
+@pytest.mark.parametrize("B,g,S,nl,det", [(2, 24, 336, 4, True), (1, 37, 518, 4, True), (3, 32, 448, 6, True),
+                                          (1, 37, 518, 6, False), (5, 24, 336, 3, False)])
+def test_partial_scores_stage_vs_float64(dev, B, g, S, nl, det):
+    """Stage 1 of aaclip_anomaly_map_partials on its own inputs: per patch row the level
+    sums of the 24 group partials, the normalised anchor dots and the level sum (and the
+    det dot for the image score) against float64 of the same partials. Ragged row counts
+    (1369 rows at 518 px: the last workgroup's 8-lane row groups run past the end), 3 / 4 /
+    6 levels, with and without the det level, a padded partials row stride; the map is
+    stage 2 (blur + upsample, the row path's band code) on the float64 grid."""
+    rows = B * g * g
+    nt = nl + int(det)
+    G = ops.SCORE_GROUPS
+    gen = torch.Generator(device=dev).manual_seed(rows + nt)
+    part = torch.full((rows, nt * 4 * G + 12), float("nan"), device=dev)  # padded stride, pad NaN
+    p = part[:, : nt * 4 * G].view(rows, nt, G, 4)
+    p[..., 0] = torch.rand(rows, nt, G, device=dev, generator=gen) * 2.0 + 0.05   # ||v||^2 group sums > 0
+    p[..., 1:3] = torch.randn(rows, nt, G, 2, device=dev, generator=gen) * 0.3
+    p[..., 3] = 0.0
+    out = torch.empty(B, S, S, device=dev)
+    grid = torch.empty(rows, device=dev)
+    dws = torch.empty(rows, device=dev) if det else None
+    score = torch.empty(B, device=dev) if det else None
+    ops.anomaly_map_partials(part, nl, out, grid, g=g, ksize=7, sigma=4.0, det_ws=dws, score=score)
+    q = p.double().sum(2)  # [rows, nt, 4]
+    inv = 1.0 / q[..., 0].sqrt().clamp_min(1e-12)
+    a0, a1 = q[..., 1] * inv, q[..., 2] * inv
+    ref_grid = ((100.0 * a1[:, :nl] + 1.0 - 100.0 * a0[:, :nl]) / 2.0).sum(1)
+    torch.testing.assert_close(grid.double(), ref_grid, rtol=1e-5, atol=1e-4)
+    ref_map = torch.empty_like(out)
+    ops.blur_upsample(ref_grid.float().view(B, 1, g, g), ref_map.view(B, 1, S, S), ksize=7, sigma=4.0)
+    torch.testing.assert_close(out, ref_map, rtol=1e-5, atol=1e-4)
+    if det:
+        torch.testing.assert_close(dws.double(), a1[:, nl], rtol=1e-5, atol=1e-6)
+        ref_score = (a1[:, nl].view(B, g * g).mean(1) + 1.0) / 2.0
+        torch.testing.assert_close(score.double(), ref_score, rtol=0, atol=1e-6)
+    # run to run: the same bits
+    grid2 = torch.empty_like(grid)
+    out2 = torch.empty_like(out)
+    ops.anomaly_map_partials(part, nl, out2, grid2, g=g, ksize=7, sigma=4.0, det_ws=dws, score=score)
+    assert torch.equal(grid, grid2) and torch.equal(out, out2)
