@@ -112,9 +112,10 @@ __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; 
 // ---------------------------------------------------------------- step timeline (diagnostic)
 // Built only with -DAACLIP_TRACE (`make trace` -> libaaclip_hip_trace.so; the product
 // library compiles none of this): every wave of an instrumented kernel appends one
-// record {t0, t1 (s_memrealtime, the chip-wide 100 MHz clock), tag, HW_ID, XCC_ID,
-// workgroup} to a caller-provided device buffer (aaclip_trace_buffer), so a tool can
-// rebuild which CU ran what when over a whole concurrent step (tools/timeline.py).
+// record {t0, t1 (s_memrealtime, the chip-wide 100 MHz clock), tag, HW_ID, XCC_ID | the
+// wave's shader-clock cycles (s_memtime delta) << 4, workgroup} to a caller-provided
+// device buffer (aaclip_trace_buffer), so a tool can rebuild which CU ran what when over
+// a whole concurrent step, and at what clock (tools/timeline.py).
 // Records go to a per-CU slab (slot = XCC, SE, SH, CU: 2048 slots) through a per-slot
 // counter 64 B apart: one counter for the whole chip serialised ~1.7 M same-address
 // atomics per step and doubled the step time. Written with vector stores after the
@@ -133,12 +134,16 @@ struct TraceState {
 };
 static __device__ TraceState g_trace;
 struct TraceScope {
-  uint64_t t0;
+  uint64_t t0, c0;
   uint32_t tag;
-  __device__ __forceinline__ explicit TraceScope(uint32_t tag_) : tag(tag_) { t0 = __builtin_amdgcn_s_memrealtime(); }
+  __device__ __forceinline__ explicit TraceScope(uint32_t tag_) : tag(tag_) {
+    t0 = __builtin_amdgcn_s_memrealtime();
+    c0 = __builtin_amdgcn_s_memtime();
+  }
   __device__ __forceinline__ ~TraceScope() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t dc = __builtin_amdgcn_s_memtime() - c0;  // shader cycles over the same span
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -149,7 +154,7 @@ struct TraceScope {
         const uint32_t wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
         uint4* r = (uint4*)(g_trace.rec + ((size_t)slot * g_trace.cap + i) * 8);
         r[0] = uint4{(uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32)};
-        r[1] = uint4{tag, hw, xcc, wg};
+        r[1] = uint4{tag, hw, (xcc & 15) | ((uint32_t)min(dc, (uint64_t)0xFFFFFFF) << 4), wg};
       }
     }
   }

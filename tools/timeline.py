@@ -2,13 +2,16 @@
 
 Loads the trace build of the library (`make -C aa-clip_amd/csrc trace` ->
 libaaclip_hip_trace.so; every wave of an instrumented kernel appends {t0, t1, tag, HW_ID,
-XCC_ID, workgroup} with t from s_memrealtime, the chip-wide 100 MHz clock), replays the
+XCC_ID | shader cycles << 4, workgroup} with t from s_memrealtime, the chip-wide 100 MHz
+clock, and the cycles an s_memtime delta over the same span), replays the
 captured C2 step (B = 32, two streams, bf16, the bench's graph) and reports, per replay:
 
   * step window (first wave start .. last wave end) and the replay's HIP-event time;
   * CU busy fraction = sum over CUs of the union of their waves' intervals / (CUs x window):
     1 - that is the share of the step in which a CU holds no wave at all (launch ramps,
     partial last tile rounds, dependent-launch gaps) -- the "gap share";
+  * per op: the in-kernel clock its waves ran at (shader cycles / real time: the DVFS clock
+    under the step's load, MI355X_MICROARCH "DVFS give-back" item 6);
   * SIMD busy fraction (the same per SIMD: a CU whose one GEMM workgroup uses all four
     SIMDs counts busy on each);
   * per op: wave-time, CU-time (union per CU of that op's waves) and the CU-time share;
@@ -76,6 +79,7 @@ def analyse(rec: np.ndarray, event_ms: float, bin_us: float = 2.0) -> dict:
     t0 = rec[:, 0].astype(np.int64) | (rec[:, 1].astype(np.int64) << 32)
     t1 = rec[:, 2].astype(np.int64) | (rec[:, 3].astype(np.int64) << 32)
     tag, hw, xcc = rec[:, 4], rec[:, 5], rec[:, 6]
+    cyc = (xcc >> 4).astype(np.int64)  # the wave's shader-clock cycles (s_memtime delta) over [t0, t1]
     lo = t0.min()
     s = (t0 - lo) / 100.0  # us (100 MHz)
     e = (t1 - lo) / 100.0
@@ -100,8 +104,11 @@ def analyse(rec: np.ndarray, event_ms: float, bin_us: float = 2.0) -> dict:
     for i, o in enumerate(names):
         m = op_id == i
         cu_time = float((oe - os_)[og // 4096 == i].sum())
+        ticks = float((t1[m] - t0[m]).sum())  # 10 ns ticks
         per_op[o] = {"waves": int(m.sum()), "wave_time_ms": round(float((e[m] - s[m]).sum()) / 1e3, 3),
-                     "cu_time_ms": round(cu_time / 1e3, 3), "cu_time_share": round(cu_time / (n_cu * window), 4)}
+                     "cu_time_ms": round(cu_time / 1e3, 3), "cu_time_share": round(cu_time / (n_cu * window), 4),
+                     # in-kernel clock over the op's waves: shader cycles / elapsed real time
+                     "clock_ghz": round(float(cyc[m].sum()) / ticks * 0.1, 3) if ticks > 0 else None}
     # idle gaps per CU: before the first segment, between segments, after the last one
     first = np.ones(len(sg), bool)
     first[1:] = sg[1:] != sg[:-1]
@@ -137,6 +144,7 @@ def analyse(rec: np.ndarray, event_ms: float, bin_us: float = 2.0) -> dict:
                                "frac_time_under_90pct": round(float((occ < 0.9 * n_cu).mean()), 4),
                                "bins": [round(float(v), 1) for v in occ]},
         "per_op": per_op,
+        "clock_ghz_all_waves": round(float(cyc.sum()) / float((t1 - t0).sum()) * 0.1, 3),
     }
 
 
