@@ -803,9 +803,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
 // its last read (WAR) and lands 5-6 phases before it is read; each phase's
 // vmcnt(8) (4 regions of 2 DMAs in flight) retires the region the next phase
 // reads (RAW: read one phase after the wait, past both groups' barriers).
-// Loads past the last K-step re-read its columns into regions nobody reads again,
-// so the vmcnt arithmetic stays uniform. Operands via buffer descriptors (rows >= M
-// read as zero; outputs dropped by the epilogue's bound check).
+// The last two K-steps issue nothing past the end and count their waits down (below).
+// Operands via buffer descriptors (rows >= M read as zero; outputs dropped by the
+// epilogue's bound check).
 // (A persistent form -- one workgroup per CU walking tiles, the next tile's first
 // K-steps fetched by the phantom loads under the epilogue -- measured -1.0 % in the C2
 // step and was removed in round 5; it is in the round-4 history, family 5.)
@@ -839,10 +839,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   int tm, tn;
   tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
   const int avo = a_vo_of(tm * BM), wvo = w_vo_of(tn * BN);
-  // region r of K-step kt into stage kt&1 (r: 0 = A0, 1 = A1, 2 = B0, 3 = B1); kt >= nk
-  // is a phantom re-read of the last one
+  // region r of K-step kt into stage kt&1 (r: 0 = A0, 1 = A1, 2 = B0, 3 = B1)
   auto issue = [&](int r, int kt) {
-    const int kc = min(kt, nk - 1) * 128;
+    const int kc = kt * 128;
     char* dst = smem + (kt & 1) * STAGE + r * REGION;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -879,9 +878,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   issue(2, 0);
   issue(3, 0);
   issue(1, 0);
-  issue(0, 1);
-  issue(2, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0(0), B0(0) landed
+  if (nk > 1) {
+    issue(0, 1);
+    issue(2, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0(0), B0(0) landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // one K-step: B1(0), A1(0) may fly
+  }
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: wave row 1 runs one barrier behind
   // No s_setprio flips around the MFMA clusters (the sched_barrier fences already pin each
@@ -911,8 +914,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       for (int kk = 0; kk < 2; ++kk)
         bfr[q][j][kk] = *(const V8*)(st + q * REGION + b_rd[kk] + j * 2048);
   };
-#define PH_SYNC_MFMA(QA, QB)                                 \
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");           \
+#define PH_SYNC_MFMA(QA, QB, W)                              \
+  asm volatile("s_waitcnt vmcnt(" #W ")" ::: "memory");      \
   __builtin_amdgcn_s_barrier();                              \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
   __builtin_amdgcn_sched_barrier(0);                         \
@@ -932,33 +935,45 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   for (int i = 0; i < RM; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* st = smem + (kt & 1) * STAGE;
-    // P1: A0 x B0
-    read_b(st, 0);
-    read_a(st, 0);
-    issue(3, kt + 1);
-    PH_SYNC_MFMA(0, 0)
-    // P2: A0 x B1
-    read_b(st, 1);
-    issue(1, kt + 1);
-    PH_SYNC_MFMA(0, 1)
-    // P3: A1 x B1
-    read_a(st, 1);
-    issue(0, kt + 2);
-    PH_SYNC_MFMA(1, 1)
-    // P4: A1 x B0
-    issue(2, kt + 2);
-    PH_SYNC_MFMA(1, 0)
+  // One K-step: P1 A0 x B0, P2 A0 x B1, P3 A1 x B1, P4 A1 x B0, each phase's counted wait
+  // W1..W4; I1 / I2: the K-step issues its regions of K-steps kt+1 / kt+2.
+#define PH_KSTEP(KT, W1, W2, W3, W4, I1, I2)        \
+  {                                                 \
+    const char* st = smem + ((KT) & 1) * STAGE;     \
+    read_b(st, 0);                                  \
+    read_a(st, 0);                                  \
+    if (I1) issue(3, (KT) + 1);                     \
+    PH_SYNC_MFMA(0, 0, W1)                          \
+    read_b(st, 1);                                  \
+    if (I1) issue(1, (KT) + 1);                     \
+    PH_SYNC_MFMA(0, 1, W2)                          \
+    read_a(st, 1);                                  \
+    if (I2) issue(0, (KT) + 2);                     \
+    PH_SYNC_MFMA(1, 1, W3)                          \
+    if (I2) issue(2, (KT) + 2);                     \
+    PH_SYNC_MFMA(1, 0, W4)                          \
   }
+  int kt = 0;
+  for (; kt < nk - 2; ++kt) PH_KSTEP(kt, 8, 8, 8, 8, true, true)
+  // The last two K-steps issue nothing past the last K-step: in K-step nk-2 P3 / P4 issue
+  // nothing, so P4 waits for A0 / B0 of nk-1 with only B1 / A1 of nk-1 left in flight
+  // (vmcnt 4); in K-step nk-1 P1 leaves A1 (vmcnt 2) and P2 drains. (Until round 5 the
+  // steady-state body ran to the end with phantom re-reads of the last K-step -- 1.5 K-steps
+  // of DMA per tile nobody read, still in flight ahead of the epilogue's own loads.)
+  if (nk >= 2) {
+    PH_KSTEP(kt, 8, 8, 8, 4, true, false)
+    ++kt;
+  }
+  PH_KSTEP(kt, 2, 0, 0, 0, false, false)
+#undef PH_KSTEP
   // both wave rows run the epilogue together (row 0 waits out row 1's last phase)
   if (wr == 0) __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");  // the epilogue's LDS slot writes stay behind that barrier
   const int mw = m0 + wr * TM, nw = n0 + wc * TN;
   const float* lbp = (const float*)(smem + 2 * STAGE) - n0;  // staged bias, by column
   // the epilogue's per-wave 4-KiB LDS slot: regions A1 / B1 of the last K-step's stage,
-  // whose last reads (P3 / P2) every wave finished before the barrier above and which
-  // no phantom DMA targets (those fill the other stage and this stage's A0 / B0)
+  // whose last reads (P3 / P2) every wave finished before the barrier above (no DMA is
+  // issued after the last K-step's regions)
   char* slot = smem + ((nk - 1) & 1) * STAGE + (wr ? 3 : 1) * REGION + wc * 4096;
   if (stamp) ts[1] = __builtin_amdgcn_s_memtime();
   if (a.dbg & 1) {
@@ -992,7 +1007,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   }
 #undef PH_SYNC_MFMA
   if (stamp) ts[2] = __builtin_amdgcn_s_memtime();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phantom loads drained before exit
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every load / store retired before exit
   if (stamp) {
     ts[3] = __builtin_amdgcn_s_memtime();
     if (lane < 4) ((uint64_t*)a.aux)[((size_t)blockIdx.x * 8 + wid) * 4 + lane] = ts[lane];
@@ -1035,7 +1050,7 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
   const int a_row = (int)a.lda, w_row = (int)a.ldw;
   const int nk = a.K / 128;
   auto issue = [&](int r, int kt) {
-    const int kc = min(kt, nk - 1) * 128;
+    const int kc = kt * 128;
     char* dst = smem + (kt & 1) * STAGE + r * REGION;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -1051,7 +1066,7 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
   // scratch. Branch-free on purpose: a branch here splits the loop body into two
   // blocks and the (memory-free) MFMAs then get sunk across the phase barriers.
   auto issue_sc = [&](int kt, int slot) {
-    const int kc = min(kt, nk - 1);
+    const int kc = kt;
     const int lo = (int)(wid < 2);
     const int off = lo * (slot * SC_SLOT + wid * 256) + (1 - lo) * (3 * SC_SLOT + (wid - 2) * 256);
     char* dst = smem + SCB + off;
@@ -1079,10 +1094,14 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
   issue(2, 0);
   issue(3, 0);
   issue(1, 0);
-  issue(0, 1);
-  issue_sc(1, 1);
-  issue(2, 1);
-  asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // A0(0), SC(0), B0(0) landed
+  if (nk > 1) {
+    issue(0, 1);
+    issue_sc(1, 1);
+    issue(2, 1);
+    asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // A0(0), SC(0), B0(0) landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // one K-step: B1(0), A1(0) may fly
+  }
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();
 
@@ -1112,8 +1131,8 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
             bfr[qb][j], af[i], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0, 127, 0, sa[i]);
     __builtin_amdgcn_s_setprio(0);
   };
-#define PH_SYNC_MFMA(QA, QB)                                 \
-  asm volatile("s_waitcnt vmcnt(9)" ::: "memory");           \
+#define PH_SYNC_MFMA(QA, QB, W)                              \
+  asm volatile("s_waitcnt vmcnt(" #W ")" ::: "memory");      \
   __builtin_amdgcn_s_barrier();                              \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
   __builtin_amdgcn_sched_barrier(0);                         \
@@ -1122,24 +1141,39 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
   __builtin_amdgcn_s_barrier();
 
   int slot = 0, slot2 = 2;  // kt % 3, (kt + 2) % 3
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* st = smem + (kt & 1) * STAGE;
-    read_b(st, 0);  // P1: A0 x B0
-    read_a(st, 0, slot);
-    issue(3, kt + 1);
-    PH_SYNC_MFMA(0, 0)
-    read_b(st, 1);  // P2: A0 x B1
-    issue(1, kt + 1);
-    PH_SYNC_MFMA(0, 1)
-    read_a(st, 1, slot);  // P3: A1 x B1
-    issue(0, kt + 2);
-    issue_sc(kt + 2, slot2);
-    PH_SYNC_MFMA(1, 1)
-    issue(2, kt + 2);  // P4: A1 x B0
-    PH_SYNC_MFMA(1, 0)
-    slot = slot == 2 ? 0 : slot + 1;
-    slot2 = slot2 == 2 ? 0 : slot2 + 1;
+  // one K-step with its four counted waits; I1 / I2: it issues K-step kt+1's / kt+2's
+  // regions (compile-time constants at every use: no branch splits the body)
+#define MX_KSTEP(KT, W1, W2, W3, W4, I1, I2)        \
+  {                                                 \
+    const char* st = smem + ((KT) & 1) * STAGE;     \
+    read_b(st, 0); /* P1: A0 x B0 */                \
+    read_a(st, 0, slot);                            \
+    if (I1) issue(3, (KT) + 1);                     \
+    PH_SYNC_MFMA(0, 0, W1)                          \
+    read_b(st, 1); /* P2: A0 x B1 */                \
+    if (I1) issue(1, (KT) + 1);                     \
+    PH_SYNC_MFMA(0, 1, W2)                          \
+    read_a(st, 1, slot); /* P3: A1 x B1 */          \
+    if (I2) {                                       \
+      issue(0, (KT) + 2);                           \
+      issue_sc((KT) + 2, slot2);                    \
+    }                                               \
+    PH_SYNC_MFMA(1, 1, W3)                          \
+    if (I2) issue(2, (KT) + 2); /* P4: A1 x B0 */   \
+    PH_SYNC_MFMA(1, 0, W4)                          \
+    slot = slot == 2 ? 0 : slot + 1;                \
+    slot2 = slot2 == 2 ? 0 : slot2 + 1;             \
   }
+  int kt = 0;
+  for (; kt < nk - 2; ++kt) MX_KSTEP(kt, 9, 9, 9, 9, true, true)
+  // the last two K-steps issue nothing past the end (as the bf16 kernel): P4 of K-step nk-2
+  // leaves B1 / A1 of nk-1 in flight (vmcnt 4), P1 of nk-1 only A1 (2), P2 drains
+  if (nk >= 2) {
+    MX_KSTEP(kt, 9, 9, 9, 4, true, false)
+    ++kt;
+  }
+  MX_KSTEP(kt, 2, 0, 0, 0, false, false)
+#undef MX_KSTEP
 #undef PH_SYNC_MFMA
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) __builtin_amdgcn_s_barrier();
@@ -1155,7 +1189,7 @@ __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
   const int key = a.epi;
   const int outm = a.out_dtype == AACLIP_F32 ? 0 : (a.out_dtype == AACLIP_BF16 ? 1 : 2);
   // quad-coalesced epilogue through the same per-wave LDS slot as the bf16 8-phase
-  // kernel (A1 / B1 of the last K-step's stage: no phantom DMA lands there)
+  // kernel (A1 / B1 of the last K-step's stage: no DMA lands there after their last reads)
   char* eslot = smem + ((nk - 1) & 1) * STAGE + (wr ? 3 : 1) * REGION + wc * 4096;
 #define EPI_CASE(OM, E)                                                         \
   if (outm == (OM) && key == (E)) {                                             \

@@ -1,6 +1,6 @@
 """One C5 timing line for the library AACLIP_LIB points at (bench.c5_leg: fp8 on the MLP,
 fp8 on every block GEMM, bf16; graphed two-stream predict at 448 px, batch 32), for
-interleaved library A/B rounds (tools/gpu_r04p.sh).
+interleaved library A/B rounds (tools/gpu_ab.sh).
 usage: AACLIP_LIB=path python tools/c5_ab.py [--steps 10]"""
 import argparse
 import os
