@@ -3,7 +3,8 @@ in ONE process and timed in interleaved rounds. An arm is `name=N:K:fam,N:K:fam,
 chunk's block-GEMM shape (rows = the chunk's B*577, N, K) pinned to tile family `fam`
 (aaclip_gemm_pin; pins are read at launch, so each capture keeps its own). Same bits in
 every arm (every family accumulates K in the same order) -- checked against arm 0.
-usage: python tools/step_arms.py base= outproj=1024:1024:10 nk1024=1024:1024:10,1024:4096:10"""
+usage: python tools/step_arms.py base= outproj=1024:1024:8 nk1024=1024:1024:8,1024:4096:8
+       [--img-size 448 --levels 4,8,12,16,20,24 --dtype bf16|fp8]  (config C5; fp8 pins only the bf16 GEMMs)"""
 import argparse
 import os
 import sys
@@ -23,11 +24,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--img-size", type=int, default=336)
+    ap.add_argument("--levels", default="6,12,18,24")
+    ap.add_argument("--dtype", choices=("bf16", "fp8"), default="bf16")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    vp, ad = synthetic_visual_weights(dev)
-    eng = VisualEngine(vp, ad, dtype=torch.bfloat16)
-    B, S = 32, 336
+    B, S = 32, a.img_size
+    lv = tuple(int(v) for v in a.levels.split(","))
+    vp, ad = synthetic_visual_weights(dev, seed=S, n_levels=len(lv), n_tok=(S // 14) ** 2 + 1)
+    eng = VisualEngine(vp, ad, levels=lv, dtype=torch.bfloat16 if a.dtype == "bf16" else torch.float8_e4m3fn)
     rows = (B // a.streams) * ((S // 14) ** 2 + 1)
     g = torch.Generator(device=dev).manual_seed(111)
     x = torch.randn(B, 3, S, S, device=dev, generator=g)
