@@ -37,7 +37,7 @@ from aaclip.engine import VisualEngine  # noqa: E402
 
 KIND = {1: "gemm_8ph", 2: "gemm_tile", 3: "gemm_fp8mx", 4: "attention", 5: "layernorm", 6: "block_tail",
         7: "embed_ln", 8: "im2col", 9: "map_partials", 10: "map_blur_score", 11: "gemm_f32", 12: "attn_f32",
-        13: "patch_scores", 14: "blur", 15: "det", 16: "map_fused"}
+        13: "patch_scores", 14: "blur", 15: "det"}
 EPI_BIAS, EPI_GELU, EPI_LEAKY, EPI_RESID = 1, 2, 4, 8
 
 
