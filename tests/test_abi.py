@@ -49,6 +49,10 @@ def test_argument_validation_rejects_without_launch():
     assert lib.aaclip_patch_scores(1, lv, 1, 768, ctypes.c_void_p(16), 4, 512, 1, 0, 0, ctypes.c_void_p(16), None) == 1
     with pytest.raises(RuntimeError):
         _lib.check(1, "aaclip_gemm")
+    # the product library has no trace scopes: arming a trace buffer is refused (make trace builds them)
+    if not os.environ.get("AACLIP_LIB"):
+        assert lib.aaclip_trace_buffer(f16, f16, 16) == 1
+        assert lib.aaclip_trace_buffer(None, None, 0) == 1
 
 
 def test_product_path_does_not_import_the_oracle():
