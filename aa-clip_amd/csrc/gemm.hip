@@ -918,16 +918,44 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   asm volatile("s_waitcnt vmcnt(" #W ")" ::: "memory");      \
   __builtin_amdgcn_s_barrier();                              \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
+  PHASE_STAMP_A                                              \
   __builtin_amdgcn_sched_barrier(0);                         \
   mfma_q(QA, QB);                                            \
   __builtin_amdgcn_sched_barrier(0);                         \
-  __builtin_amdgcn_s_barrier();
+  PHASE_STAMP_B                                              \
+  __builtin_amdgcn_s_barrier();                              \
+  PHASE_STAMP_STORE
 
   const bool bf16_out = a.out_dtype != AACLIP_F32;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
   // diagnostic stamps (variant bit 11): shader-clock s_memtime at kernel start, main-loop
   // end, epilogue issued, epilogue stores complete -> a.aux
   const bool stamp = (a.dbg & 4) && a.aux && !(a.epi & AACLIP_EPI_AUX_BF16);
+#ifdef AACLIP_PHASE_STAMPS
+  // diagnostic build (tools/ab_build.sh ... -DAACLIP_PHASE_STAMPS, tools/gemm_phase_stamps.py): every
+  // wave stamps s_memtime at the start and the end of each MFMA cluster of K-steps 4..11 (taken right
+  // after the pre-cluster lgkmcnt(0) and the cluster, stored to LDS after the trailing barrier, where
+  // no LDS read is outstanding), copied to a.aux at the end in place of the 4 stamps of variant bit 11
+  constexpr int kPS0 = 4, kPSN = 8;  // K-steps stamped
+  uint64_t* const ps_lds = (uint64_t*)(smem + 2 * STAGE + 1024) + wid * kPSN * 4 * 2;
+  int ps_i = 0;  // phase index since kernel start
+  uint64_t ps_a = 0, ps_b = 0;
+#define PHASE_STAMP_A ps_a = __builtin_amdgcn_s_memtime();
+#define PHASE_STAMP_B ps_b = __builtin_amdgcn_s_memtime();
+#define PHASE_STAMP_STORE                                                                   \
+  {                                                                                         \
+    const int q_ = ps_i - 4 * kPS0;                                                         \
+    if (q_ >= 0 && q_ < 4 * kPSN && lane == 0) {                                            \
+      ps_lds[2 * q_] = ps_a;                                                                \
+      ps_lds[2 * q_ + 1] = ps_b;                                                            \
+    }                                                                                       \
+    ++ps_i;                                                                                 \
+  }
+#else
+#define PHASE_STAMP_A
+#define PHASE_STAMP_B
+#define PHASE_STAMP_STORE
+#endif
   uint64_t ts[4] = {0, 0, 0, 0};
   if (stamp) ts[0] = __builtin_amdgcn_s_memtime();
   const int m0 = tm * BM, n0 = tn * BN;
@@ -1006,11 +1034,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
       wave_epilogue_lds<RM, RN, 0, -1, H16>(a, acc, mw, nw, lane, lds_bias ? lbp : nullptr, slot);
   }
 #undef PH_SYNC_MFMA
+#undef PHASE_STAMP_A
+#undef PHASE_STAMP_B
+#undef PHASE_STAMP_STORE
   if (stamp) ts[2] = __builtin_amdgcn_s_memtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every load / store retired before exit
   if (stamp) {
     ts[3] = __builtin_amdgcn_s_memtime();
+#ifdef AACLIP_PHASE_STAMPS
+    if (lane < 2 * 4 * kPSN) ((uint64_t*)a.aux)[((size_t)blockIdx.x * 8 + wid) * 2 * 4 * kPSN + lane] = ps_lds[lane];
+#else
     if (lane < 4) ((uint64_t*)a.aux)[((size_t)blockIdx.x * 8 + wid) * 4 + lane] = ts[lane];
+#endif
   }
 }
 
@@ -1226,7 +1261,11 @@ int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   if (a.N % 256 || a.K % 64) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
+#ifdef AACLIP_PHASE_STAMPS
+  const size_t lds = 2 * 4 * 128 * 128 + 1024 + 8 * 8 * 4 * 2 * 8;  // + the phase stamps (diagnostic build)
+#else
   const size_t lds = 2 * 4 * 128 * 128 + 1024;  // the ring + the tile's bias
+#endif
   static unsigned attr_dev = 0;
   if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, SCORES>, (int)lds, attr_dev))
     return AACLIP_ERR_LAUNCH;
