@@ -934,23 +934,25 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
 #ifdef AACLIP_PHASE_STAMPS
   // diagnostic build (tools/ab_build.sh ... -DAACLIP_PHASE_STAMPS, tools/gemm_phase_stamps.py): every
   // wave stamps s_memtime at the start and the end of each MFMA cluster of K-steps 4..11 (taken right
-  // after the pre-cluster lgkmcnt(0) and the cluster, stored to LDS after the trailing barrier, where
-  // no LDS read is outstanding), copied to a.aux at the end in place of the 4 stamps of variant bit 11
+  // after the pre-cluster lgkmcnt(0) and after the cluster), kept in LDS and copied to a.aux at the end
+  // in place of the 4 stamps of variant bit 11 (needs K >= 768)
   constexpr int kPS0 = 4, kPSN = 8;  // K-steps stamped
   uint64_t* const ps_lds = (uint64_t*)(smem + 2 * STAGE + 1024) + wid * kPSN * 4 * 2;
   int ps_i = 0;  // phase index since kernel start
   uint64_t ps_a = 0, ps_b = 0;
-#define PHASE_STAMP_A ps_a = __builtin_amdgcn_s_memtime();
-#define PHASE_STAMP_B ps_b = __builtin_amdgcn_s_memtime();
-#define PHASE_STAMP_STORE                                                                   \
+  // the previous phase's pair is stored at the next cluster start, right after that phase's
+  // lgkmcnt(0) has retired both s_memtime reads: the stamps add no wait of their own
+#define PHASE_STAMP_A                                                                       \
   {                                                                                         \
-    const int q_ = ps_i - 4 * kPS0;                                                         \
+    const int q_ = ps_i - 1 - 4 * kPS0;                                                     \
     if (q_ >= 0 && q_ < 4 * kPSN && lane == 0) {                                            \
       ps_lds[2 * q_] = ps_a;                                                                \
       ps_lds[2 * q_ + 1] = ps_b;                                                            \
     }                                                                                       \
-    ++ps_i;                                                                                 \
+    ps_a = __builtin_amdgcn_s_memtime();                                                    \
   }
+#define PHASE_STAMP_B ps_b = __builtin_amdgcn_s_memtime();
+#define PHASE_STAMP_STORE ++ps_i;
 #else
 #define PHASE_STAMP_A
 #define PHASE_STAMP_B
