@@ -75,22 +75,42 @@ SIGNATURES = {
 _lib = None
 
 
+def load(path: str) -> ctypes.CDLL:
+    """Open an aaclip library and bind every SIGNATURES entry. The version check comes
+    BEFORE any other symbol is bound: a stale library (built from older sources, missing
+    newer entry points) is refused with one clear RuntimeError instead of an
+    AttributeError at the first call of a symbol it lacks."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} is missing: the HIP kernels are not built "
+            "(run `python __graft_entry__.py` or `make -C aa-clip_amd/csrc`). "
+            "There is no CPU fallback.")
+    handle = ctypes.CDLL(path)
+    try:
+        ver = handle.aaclip_abi_version
+    except AttributeError:
+        raise RuntimeError(f"{path} exports no aaclip_abi_version: not an aaclip library; rebuild it "
+                           "(`make -C aa-clip_amd/csrc`)") from None
+    ver.argtypes, ver.restype = [], ctypes.c_int
+    found = ver()
+    if found != ABI_VERSION:
+        raise RuntimeError(f"{path} has ABI version {found}, this package needs {ABI_VERSION}: the library "
+                           "is stale; rebuild it (`make -C aa-clip_amd/csrc`)")
+    missing = [name for name in SIGNATURES if not hasattr(handle, name)]
+    if missing:
+        raise RuntimeError(f"{path} (ABI {found}) lacks {', '.join(missing)}: the library is stale; "
+                           "rebuild it (`make -C aa-clip_amd/csrc`)")
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_char_p if name in ("aaclip_arch", "aaclip_gemm_plan") else ctypes.c_int
+    return handle
+
+
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(
-                f"{LIB_PATH} is missing: the HIP kernels are not built "
-                "(run `python __graft_entry__.py` or `make -C aa-clip_amd/csrc`). "
-                "There is no CPU fallback.")
-        handle = ctypes.CDLL(LIB_PATH)
-        for name, argtypes in SIGNATURES.items():
-            fn = getattr(handle, name)
-            fn.argtypes = argtypes
-            fn.restype = ctypes.c_char_p if name in ("aaclip_arch", "aaclip_gemm_plan") else ctypes.c_int
-        if handle.aaclip_abi_version() != ABI_VERSION:
-            raise RuntimeError("libaaclip_hip.so ABI version mismatch; rebuild it")
-        _lib = handle
+        _lib = load(LIB_PATH)
     return _lib
 
 

@@ -113,8 +113,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
 
 
 # tile families aaclip_gemm_pin accepts (include/aaclip.h): 8-phase 256x256, 320x256,
-# 256x256, 128x128, 256x128, two-workgroup 256x128, 64x64
-GEMM_FAMILIES = (3, 8, 1, 9, 2, 10, 11)
+# 256x256, 128x128, 256x128, 64x64 (the two-workgroup family 10 was removed in round 5)
+GEMM_FAMILIES = (3, 8, 1, 9, 2, 11)
 _tuned = {}
 
 
@@ -122,8 +122,6 @@ def _family_applies(fam: int, N: int, K: int) -> bool:
     """The shapes aaclip_gemm_pin / choose16 honour a family on (else it falls back)."""
     if fam in (1, 3, 8, 9):
         return N % 256 == 0
-    if fam == 10:
-        return K % 32 == 0
     if fam == 11:
         return N % 64 == 0
     return True  # 0 (the unpinned per-shape heuristic) and 2

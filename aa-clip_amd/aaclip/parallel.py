@@ -84,21 +84,23 @@ def verify_gather(predict, images_of, s_all: torch.Tensor, s_local: torch.Tensor
                                                                  "checked_by": checker}}
 
 
-def gather_rows_to(local: torch.Tensor, n_total: int, dst: int = 0, group=None):
+def gather_rows_to(local: torch.Tensor, n_total: int, dst: int = 0, group=None, host_staging=None):
     """Gather variable-size row shards (shard_range order) onto rank `dst` only: returns
     the global [n_total, ...] tensor there and None on the other ranks. For results only
     one rank consumes (the harness's pixel maps before metrics_eval): 1/world of
     gather_rows' receive traffic. An empty local shard (n_total < world) still takes
-    part, with zero rows of the right shape."""
+    part, with zero rows of the right shape.
+    host_staging: None = by backend (gloo's gather takes host tensors only -- the one-GPU
+    rehearsal of the multi-rank harness, every rank on cuda:0 over gloo; RCCL gathers
+    device memory directly); False = gather `local` where it lives (the RCCL branch; the
+    CPU tests force it with host tensors over gloo), True = stage through host memory."""
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     if world == 1:
         return local
     rank = dist.get_rank(group)
     sizes = [shard_range(n_total, r, world) for r in range(world)]
     width = max(b - a for a, b in sizes)
-    # gloo's gather takes host tensors only (the one-GPU rehearsal of the multi-rank harness:
-    # every rank on cuda:0 over gloo); RCCL gathers device memory directly
-    host = str(dist.get_backend(group)) == "gloo"
+    host = str(dist.get_backend(group)) == "gloo" if host_staging is None else bool(host_staging)
     pad = torch.zeros((width,) + tuple(local.shape[1:]), device="cpu" if host else local.device, dtype=local.dtype)
     pad[: local.shape[0]] = local
     bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None

@@ -56,6 +56,13 @@ struct GemmArgs {
 // out_dtype tag of the score-partials output (aaclip_gemm_scores; never a public dtype)
 constexpr int kOutScores = 100;
 
+// trace-build tag of a GEMM launch: N/64 in bits 4-11, K/64 in bits 12-19 (each capped at
+// 255, so N or K >= 16384 saturates its field instead of spilling into the next), epilogue
+// flags from bit 20 (diagnostic builds only; tools/timeline.py decodes it)
+__host__ __device__ inline uint32_t gemm_trace_tag(const GemmArgs& a) {
+  return (uint32_t)min(a.N / 64, 255) << 4 | (uint32_t)min(a.K / 64, 255) << 12 | (uint32_t)a.epi << 20;
+}
+
 // smallest e with amax * 2^-e <= 448 (largest finite e4m3): the e8m0 block scale
 __device__ __forceinline__ int mx_exp(float amax) {
   if (!(amax > 0.f)) return 0;
@@ -542,7 +549,7 @@ typedef __attribute__((ext_vector_type(4))) int i32x4_t;
 // H16 (Q == 0 only): fp16 operands on v_mfma_f32_16x16x32_f16 (same tiles and cycles).
 template <int BM, int BN, int WM, int WN, int Q = 0, bool H16 = false>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
-  AACLIP_TRACE_SCOPE(TR_GEMM_TILE | (uint32_t)(a.N / 64) << 4 | (uint32_t)(a.K / 64) << 12 | (uint32_t)a.epi << 20);
+  AACLIP_TRACE_SCOPE(TR_GEMM_TILE | gemm_trace_tag(a));
   static_assert(!H16 || Q == 0, "fp16 operands: 16-bit path only");
   constexpr bool FP8 = Q != 0, MX = Q == 2;
   constexpr int NWAVES = WM * WN;
@@ -732,7 +739,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
 
 // ============================================================== fp32 MFMA kernel
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
-  AACLIP_TRACE_SCOPE(TR_GEMM_F32 | (uint32_t)(a.N / 64) << 4 | (uint32_t)(a.K / 64) << 12 | (uint32_t)a.epi << 20);
+  AACLIP_TRACE_SCOPE(TR_GEMM_F32 | gemm_trace_tag(a));
   constexpr int BM = 64, BN = 64, BK = 16, LDK = BK + 1;
   __shared__ float As[BM][LDK];
   __shared__ float Bs[BN][LDK];
@@ -813,7 +820,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
 // anomaly-map partials path adds no registers to the block-GEMM instantiations.
 template <bool H16, bool SCORES = false>
 __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
-  AACLIP_TRACE_SCOPE(TR_GEMM_8PH | (uint32_t)(a.N / 64) << 4 | (uint32_t)(a.K / 64) << 12 | (uint32_t)a.epi << 20);
+  AACLIP_TRACE_SCOPE(TR_GEMM_8PH | gemm_trace_tag(a));
   using V8 = h16x8_t<H16>;
   constexpr int BM = 256, BN = 256, TM = 128, TN = 64, RM = 8, RN = 4;
   constexpr int REGION = 128 * 128;                 // bytes per LDS region
@@ -1060,7 +1067,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
 // (2, 2, 3, 2) are uniform and any 4 consecutive phases hold 9 -> vmcnt(9). Slot
 // (k+2)%3 is rewritten at P3(k), 4 phases after K-step k-1's last scale read.
 __global__ __launch_bounds__(512) void gemm_fp8mx_8ph_kernel(GemmArgs a) {
-  AACLIP_TRACE_SCOPE(TR_GEMM_FP8MX | (uint32_t)(a.N / 64) << 4 | (uint32_t)(a.K / 64) << 12 | (uint32_t)a.epi << 20);
+  AACLIP_TRACE_SCOPE(TR_GEMM_FP8MX | gemm_trace_tag(a));
   constexpr int BM = 256, BN = 256, TM = 128, TN = 64, RM = 8, RN = 4;
   constexpr int REGION = 128 * 128;
   constexpr int STAGE = 4 * REGION;

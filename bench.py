@@ -699,6 +699,35 @@ def cpu_baseline_and_parity(dev, streams: int, min_seconds: float = 12.0, warmup
     return base, parity
 
 
+def parity_stats(grid, maps, scores, ref_grid, ref_maps, ref_scores, lab, auc_cpu=None):
+    """One compute mode's outputs against the CPU oracle's on the same images (pure numpy):
+    grid [n, L, P, 2] = 100 f.T per (image, level, patch), maps [n, S, S], scores [n];
+    lab = the pixel labels for the AUROC. The fields the parity gate reads."""
+    import numpy as np
+    from sklearn.metrics import roc_auc_score
+    if auc_cpu is None:
+        auc_cpu = float(roc_auc_score(lab, ref_maps.reshape(-1)))
+    tol = 1e-3 + 1e-2 * np.abs(ref_maps)
+    margin = np.abs(ref_grid[..., 1] - ref_grid[..., 0])
+    sure = margin > 1e-3
+    err = np.abs(maps - ref_maps)
+    flips = grid.argmax(-1) != ref_grid.argmax(-1)
+    finite = bool(np.isfinite(maps).all() and np.isfinite(scores).all() and np.isfinite(grid).all())
+    auc_gpu = float(roc_auc_score(lab, maps.reshape(-1))) if finite else float("nan")
+    # per level (grid axis 1): a kernel change that doubles one level's flips shows here
+    per_level = [int(flips[:, lv][sure[:, lv]].sum()) for lv in range(flips.shape[1])]
+    return {"patch_label_flips_sure": int(flips[sure].sum()), "patch_label_flips_all": int(flips.sum()),
+            "patch_label_flips_sure_per_level": per_level,
+            "patch_label_flip_rate_sure": round(float(flips[sure].mean()), 6) if sure.any() else 0.0,
+            "anchor_logit_max_abs_err": float(np.abs(grid - ref_grid).max()),
+            "pixel_auroc_gpu": round(auc_gpu, 6), "pixel_auroc_abs_diff": abs(auc_gpu - auc_cpu) if finite else 1.0,
+            "map_max_abs_err": float(err.max()) if finite else float("inf"),
+            "map_within_tol": bool((err <= tol).all()),
+            "frac_pixels_within_tol": float((err <= tol).mean()),
+            "image_score_max_abs_err": float(np.abs(scores - ref_scores).max()) if finite else float("inf"),
+            "image_labels_equal": bool(np.array_equal(scores > 0.5, ref_scores > 0.5)), "finite": finite}
+
+
 def _parity_size(dev, streams, S, sd, ia, x, T, refs, synth):
     import numpy as np
     from sklearn.metrics import roc_auc_score
@@ -709,11 +738,9 @@ def _parity_size(dev, streams, S, sd, ia, x, T, refs, synth):
     masks = synth.masks(111, n, S)[:, 0]
     lab = masks.reshape(-1) > 0
     auc_cpu = float(roc_auc_score(lab, ref_maps.reshape(-1)))
-    tol = 1e-3 + 1e-2 * np.abs(ref_maps)
     margin = np.abs(ref_grid[..., 1] - ref_grid[..., 0])
-    sure = margin > 1e-3
     out = {"pixel_auroc_cpu_ref": round(auc_cpu, 6), "patch_labels": int(margin.size),
-           "patch_labels_sure": int(sure.sum())}
+           "patch_labels_sure": int((margin > 1e-3).sum())}
     vp = {k: torch.from_numpy(v).to(dev) for k, v in sd.items() if k.startswith("visual.")}
     iad = {k: torch.from_numpy(v).to(dev) for k, v in ia.items()}
     xs, Td = x.to(dev), torch.from_numpy(T).to(dev)
@@ -722,24 +749,148 @@ def _parity_size(dev, streams, S, sd, ia, x, T, refs, synth):
         seg, _ = eng.forward(xs)
         grid = torch.stack([100.0 * (f @ Td) for f in seg], 1).cpu().numpy()
         m, sc = eng.predict(xs, Td, "Industrial", streams=streams)
-        gpu_maps, gpu_scores = m.cpu().numpy(), sc.cpu().numpy()
-        err = np.abs(gpu_maps - ref_maps)
-        flips = grid.argmax(-1) != ref_grid.argmax(-1)
-        auc_gpu = float(roc_auc_score(lab, gpu_maps.reshape(-1)))
-        # per level (grid axis 1): a kernel change that doubles one level's flips shows here
-        per_level = [int(flips[:, lv][sure[:, lv]].sum()) for lv in range(flips.shape[1])]
-        out[tag] = {"patch_label_flips_sure": int(flips[sure].sum()), "patch_label_flips_all": int(flips.sum()),
-                    "patch_label_flips_sure_per_level": per_level,
-                    "patch_label_flip_rate_sure": round(float(flips[sure].mean()), 6),
-                    "anchor_logit_max_abs_err": float(np.abs(grid - ref_grid).max()),
-                    "pixel_auroc_gpu": round(auc_gpu, 6), "pixel_auroc_abs_diff": abs(auc_gpu - auc_cpu),
-                    "map_max_abs_err": float(err.max()), "map_within_tol": bool((err <= tol).all()),
-                    "frac_pixels_within_tol": float((err <= tol).mean()),
-                    "image_score_max_abs_err": float(np.abs(gpu_scores - ref_scores).max()),
-                    "image_labels_equal": bool(np.array_equal(gpu_scores > 0.5, ref_scores > 0.5))}
+        out[tag] = parity_stats(grid, m.cpu().numpy(), sc.cpu().numpy(), ref_grid, ref_maps, ref_scores, lab,
+                                auc_cpu)
         del eng, seg, m, sc
         torch.cuda.empty_cache()
     return out
+
+
+# ---------------------------------------------------------------- parity gate
+# The bounds every bench line is held to (exit status 1 and "parity_gate": false otherwise):
+# the tests' bounds (tests/test_e2e_gpu.py, test_fp16_gpu.py) applied to the bench's own
+# parity leg against the CPU oracle. bf16 sure patch-label flips: the counts this tree
+# measures on the parity leg's 8 images (per size; per level), held to 2x in total and
+# 2x + 2 per level; fp16 / fp32: the north_star contract in full (every pixel within
+# 1e-3 + 1e-2 |ref|, 0 sure flips). Reference: test.py:80-93.
+BF16_PARITY_FLIPS = {"336": (33, (4, 0, 29, 0)), "518": (87, (12, 0, 71, 4))}
+BF16_MIN_FRAC_WITHIN_TOL = 0.999
+MAX_PIXEL_AUROC_DIFF = 2e-3
+# the timed step's own outputs (images of the timed batch, the bench's own weights) vs the
+# oracle: bf16 maps, checked on every line (every N, every rank-0 shard)
+TIMED_MIN_FRAC_WITHIN_TOL = 0.99
+TIMED_MAX_MAP_REL_L2 = 1e-2
+TIMED_MAX_SCORE_ABS_ERR = 2e-3
+# C5 (448 px, 6 levels) against the fp32 parity mode of the same path
+C5_BF16_MIN_FRAC_WITHIN_TOL = 0.999
+C5_FP8_MAX_MAP_REL_L2 = 1.5e-2
+
+
+def parity_gate(line: dict) -> dict:
+    """Check a bench line's parity legs against the bounds above. Returns {"pass": bool,
+    "checked": [leg names], "failed": [reasons]}; a line with no parity leg at all fails
+    (every line carries at least timed_step_vs_oracle)."""
+    failed, checked = [], []
+    tv = line.get("timed_step_vs_oracle")
+    if tv is not None:
+        checked.append("timed_step_vs_oracle")
+        if not tv.get("finite", False):
+            failed.append("timed step: non-finite outputs")
+        if tv["frac_pixels_within_tol"] < TIMED_MIN_FRAC_WITHIN_TOL:
+            failed.append(f"timed step: {tv['frac_pixels_within_tol']:.6f} of pixels within tol "
+                          f"< {TIMED_MIN_FRAC_WITHIN_TOL}")
+        if not tv["map_rel_l2"] <= TIMED_MAX_MAP_REL_L2:
+            failed.append(f"timed step: map rel-L2 {tv['map_rel_l2']:.3e} > {TIMED_MAX_MAP_REL_L2}")
+        if not tv["image_score_max_abs_err"] <= TIMED_MAX_SCORE_ABS_ERR:
+            failed.append(f"timed step: image score err {tv['image_score_max_abs_err']:.3e} > "
+                          f"{TIMED_MAX_SCORE_ABS_ERR}")
+        if not tv["image_labels_equal"]:
+            failed.append("timed step: image labels differ")
+    par = line.get("parity")
+    if par is not None:
+        for size in par["sizes"]:
+            leg = par[str(size)]
+            for tag in ("bf16", "fp16", "fp32"):
+                r = leg[tag]
+                where = f"parity {size}px {tag}"
+                checked.append(where)
+                if not r.get("finite", True):
+                    failed.append(f"{where}: non-finite outputs")
+                if not r["image_labels_equal"]:
+                    failed.append(f"{where}: image labels differ")
+                if not r["pixel_auroc_abs_diff"] <= MAX_PIXEL_AUROC_DIFF:
+                    failed.append(f"{where}: pixel AUROC differs by {r['pixel_auroc_abs_diff']:.2e}")
+                if tag == "bf16":
+                    tot, lv = BF16_PARITY_FLIPS[str(size)]
+                    if r["patch_label_flips_sure"] > 2 * tot:
+                        failed.append(f"{where}: {r['patch_label_flips_sure']} sure flips > 2 x {tot}")
+                    got = r["patch_label_flips_sure_per_level"]
+                    if len(got) != len(lv) or any(f > 2 * m + 2 for f, m in zip(got, lv)):
+                        failed.append(f"{where}: sure flips per level {got} exceed 2 x {list(lv)} + 2")
+                    if r["frac_pixels_within_tol"] < BF16_MIN_FRAC_WITHIN_TOL:
+                        failed.append(f"{where}: {r['frac_pixels_within_tol']:.6f} of pixels within tol "
+                                      f"< {BF16_MIN_FRAC_WITHIN_TOL}")
+                else:  # fp16 / fp32: the full north_star contract
+                    if not r["map_within_tol"]:
+                        failed.append(f"{where}: map outside 1e-3 + 1e-2 |ref| (max {r['map_max_abs_err']:.3e})")
+                    if r["patch_label_flips_sure"] != 0:
+                        failed.append(f"{where}: {r['patch_label_flips_sure']} sure patch-label flips")
+    c5 = line.get("c5")
+    if c5 is not None:
+        checked.append("c5")
+        if c5["bf16"]["frac_pixels_within_fp32_contract"] < C5_BF16_MIN_FRAC_WITHIN_TOL:
+            failed.append(f"c5 bf16: {c5['bf16']['frac_pixels_within_fp32_contract']:.6f} of pixels within the "
+                          "fp32 contract")
+        if not c5["fp8"]["map_rel_l2_vs_fp32"] <= C5_FP8_MAX_MAP_REL_L2:
+            failed.append(f"c5 fp8: map rel-L2 {c5['fp8']['map_rel_l2_vs_fp32']:.3e} > {C5_FP8_MAX_MAP_REL_L2}")
+    if not checked:
+        failed.append("no parity leg in the line")
+    return {"pass": not failed, "checked": checked, "failed": failed}
+
+
+def timed_step_vs_oracle(vp, ad, x, maps, scores, T, idx=(0, -1), threads=None):
+    """The TIMED step's own outputs (the graph replay's maps / scores for images idx of this
+    rank's shard) against the CPU oracle (oracle/aaclip_torch.py, fp32) on the bench's own
+    synthetic weights and images: the line proves what it timed, not an eager re-run of the
+    same library. Runs after timing, on rank 0."""
+    import numpy as np
+
+    from oracle import aaclip_torch as RT
+    n = x.shape[0]
+    idx = sorted({i % n for i in idx})
+    cpu = lambda d: {k: v.detach().float().cpu() for k, v in d.items()}  # noqa: E731
+    w = RT.prepare(cpu(vp), cpu(ad))
+    Tc = T.detach().float().cpu()
+    t0 = time.perf_counter()
+    threads0 = torch.get_num_threads()
+    if threads:
+        torch.set_num_threads(threads)
+    ref_m, ref_s = [], []
+    with torch.no_grad():
+        for i in idx:
+            seg, det = RT.visual_forward(w, x[i:i + 1].float().cpu())
+            ref_m.append(RT.anomaly_map(seg, Tc, x.shape[-1], "Industrial")[0].numpy())
+            ref_s.append(float(RT.image_score(det, Tc)[0]))
+    torch.set_num_threads(threads0)
+    ref_m, ref_s = np.stack(ref_m), np.array(ref_s, dtype=np.float32)
+    got_m = maps[idx].float().cpu().numpy()
+    got_s = scores[idx].float().cpu().numpy()
+    finite = bool(np.isfinite(got_m).all() and np.isfinite(got_s).all())
+    err = np.abs(got_m - ref_m)
+    tol = 1e-3 + 1e-2 * np.abs(ref_m)
+    return {"images": [int(i) for i in idx], "reference": "CPU fp32 torch oracle, the bench's own weights and images",
+            "finite": finite, "map_max_abs_err": float(err.max()) if finite else float("inf"),
+            "map_rel_l2": float(np.linalg.norm(got_m - ref_m) / np.linalg.norm(ref_m)) if finite else float("inf"),
+            "frac_pixels_within_tol": float((err <= tol).mean()),
+            "image_score_max_abs_err": float(np.abs(got_s - ref_s).max()) if finite else float("inf"),
+            "image_labels_equal": bool(np.array_equal(got_s > 0.5, ref_s > 0.5)),
+            "cpu_seconds": round(time.perf_counter() - t0, 1)}
+
+
+def emit(line: dict, rank: int = 0) -> int:
+    """Gate the line on its parity legs, print it (rank 0) and return the exit status:
+    0 when every bound holds, 1 otherwise ("parity_gate": false and the reasons in
+    "parity_gate_failed")."""
+    g = parity_gate(line)
+    line["parity_gate"] = g["pass"]
+    line["parity_gate_checked"] = g["checked"]
+    if g["failed"]:
+        line["parity_gate_failed"] = g["failed"]
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+        if g["failed"]:
+            print("bench.py: PARITY GATE FAILED: " + "; ".join(g["failed"]), file=sys.stderr, flush=True)
+    return 0 if g["pass"] else 1
 
 
 def modes_leg(vp, ad, x, T, steps: int, warmup: int, streams: int):
@@ -790,6 +941,9 @@ def main():
     ap.add_argument("--no-modes", action="store_true", help="skip the fp16 / fp32 mode throughput leg")
     ap.add_argument("--gemm-variant", type=int, default=0, help="aaclip_set_gemm_variant value (A/B runs)")
     ap.add_argument("--attn-variant", type=int, default=0, help="aaclip_set_attn_variant value (A/B runs)")
+    ap.add_argument("--no-oracle-check", action="store_true",
+                    help="skip the timed step's check against the CPU oracle AND the parity gate (A/B timing runs "
+                         "only; such a line carries no parity_gate)")
     ap.add_argument("--dtype", choices=("bf16", "fp16"), default="bf16",
                     help="compute dtype of the timed step (C2 is quoted in bf16; fp16 = the contract mode, for A/B)")
     args = ap.parse_args()
@@ -907,6 +1061,10 @@ def main():
     line["step_outputs_verified"] = {
         "finite": bool(torch.isfinite(m_t).all() and torch.isfinite(s_t).all()),
         "equal_to_one_stream_eager": bool(torch.equal(m_t, m_e) and torch.equal(s_t, s_e))}
+    if rank == 0 and not args.no_oracle_check:
+        # ... and against the CPU oracle: first and last image of rank 0's shard, the timed
+        # replay's own maps / scores (parity_gate holds them to the TIMED_* bounds)
+        line["timed_step_vs_oracle"] = timed_step_vs_oracle(vp, ad, x, m_t, s_t, T)
     del m_t, s_t
     if rank == 0 and not args.no_roofline:
         # in-step per-launch durations: the one-stream step (the roofline; a rocprofv3 kernel
@@ -951,13 +1109,20 @@ def main():
         del eng, run, vp, ad
         torch.cuda.empty_cache()
         line["c5"] = c5_leg(dev, max(3, args.steps // 2), args.warmup, n_streams)
-    if rank == 0:
+    rc = emit(line, rank) if (rank == 0 and not args.no_oracle_check) else 0
+    if rank == 0 and args.no_oracle_check:
         print(json.dumps(line), flush=True)
     if world > 1:
+        # every rank leaves with rank 0's parity verdict
+        flag = torch.tensor([rc], dtype=torch.int32, device="cpu" if rehearsal else dev)
+        dist.broadcast(flag, 0)
+        rc = int(flag.item())
         dist.barrier()
         dist.destroy_process_group()
     if dist_check is not None and not (dist_check["gather_verified"] and dist_check["own_slice_verified"]):
         sys.exit("bench.py: the gathered image scores do not match the ranks' own / recomputed shards")
+    if rc:
+        sys.exit(rc)
 
 
 if __name__ == "__main__":

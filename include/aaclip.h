@@ -58,7 +58,8 @@ const char* aaclip_arch(void);
 /*
  * Diagnostic step timeline (trace builds only: `make trace` -> libaaclip_hip_trace.so;
  * the product library returns AACLIP_ERR_ARG). Every wave of an instrumented kernel
- * appends one record of 8 uint32 {t0 lo, t0 hi, t1 lo, t1 hi, tag, HW_ID, XCC_ID,
+ * appends one record of 8 uint32 {t0 lo, t0 hi, t1 lo, t1 hi, tag, HW_ID, word 6 = XCC_ID
+ * (bits 0-3) | the wave's s_memtime shader-cycle delta capped at 2^28-1 (bits 4-31),
  * workgroup} to the slab of its CU: slot = XCC << 8 | SE << 5 | SH << 4 | CU (2048
  * slots), records [2048][capacity][8], counter [2048][16] uint32 (slot s counts at
  * counter[16 s]; zero it before a traced run); a slot's records past capacity are

@@ -30,6 +30,36 @@ def test_library_exports_every_declared_symbol():
     assert lib.aaclip_arch() == b"gfx950"
 
 
+def _fake_lib(tmp_path, name, version, symbols=()):
+    """A stand-in shared library exporting aaclip_abi_version() (returning `version`) and
+    the given no-op symbols: what a stale build of older sources looks like to the loader."""
+    import subprocess
+    src = tmp_path / f"{name}.c"
+    body = f"int aaclip_abi_version(void) {{ return {version}; }}\n" if version is not None else ""
+    body += "".join(f"int {s}(void) {{ return 0; }}\n" for s in symbols)
+    src.write_text(body or "int unrelated_symbol(void) { return 0; }\n")
+    out = tmp_path / f"{name}.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(out), str(src)], check=True)
+    return str(out)
+
+
+def test_stale_library_is_refused_with_one_clear_error(tmp_path):
+    """_lib.load checks aaclip_abi_version BEFORE binding anything else (round 5: new Python
+    against a stale .so surfaced as AttributeErrors in 20+ tests): a wrong version, a
+    right version with missing entry points, and a foreign library each raise ONE
+    RuntimeError that names the problem; the real library loads."""
+    others = [s for s in _lib.SIGNATURES if s != "aaclip_abi_version"]
+    with pytest.raises(RuntimeError, match=r"ABI version 5, this package needs"):
+        _lib.load(_fake_lib(tmp_path, "old", 5, others))
+    with pytest.raises(RuntimeError, match=r"lacks aaclip_trace_buffer.*stale"):
+        _lib.load(_fake_lib(tmp_path, "partial", _lib.ABI_VERSION, [s for s in others if s != "aaclip_trace_buffer"]))
+    with pytest.raises(RuntimeError, match=r"exports no aaclip_abi_version"):
+        _lib.load(_fake_lib(tmp_path, "foreign", None))
+    with pytest.raises(RuntimeError, match=r"missing"):
+        _lib.load(str(tmp_path / "absent.so"))
+    assert _lib.load(_lib.LIB_PATH).aaclip_abi_version() == _lib.ABI_VERSION
+
+
 def test_argument_validation_rejects_without_launch():
     lib = _lib.lib()
     # null operands / bad dtype / unsupported shapes return AACLIP_ERR_ARG (=1)
@@ -135,3 +165,14 @@ def test_gemm_concurrent_mode_is_thread_local():
             assert plan() == t320
         assert plan() == ph8
     assert plan() == t320 and seen["other"] == t320
+
+
+def test_tuner_families_are_all_pinnable():
+    """Every family ops.tune_gemm tries is one aaclip_gemm_pin accepts (host logic, no
+    launch): the removed two-workgroup family 10 is refused and no longer listed."""
+    from aaclip import ops
+    lib = _lib.lib()
+    for fam in ops.GEMM_FAMILIES:
+        assert lib.aaclip_gemm_pin(_lib.BF16, 1234, 1024, 1024, fam) == 0, fam
+        assert lib.aaclip_gemm_pin(_lib.BF16, 1234, 1024, 1024, 0) == 0
+    assert 10 not in ops.GEMM_FAMILIES and lib.aaclip_gemm_pin(_lib.BF16, 1234, 1024, 1024, 10) == 1

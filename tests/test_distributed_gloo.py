@@ -151,3 +151,40 @@ def test_gloo_world2_sharded_step_and_harness(n):
             continue
         assert mk_sum == ref[0].sum().item() and labels == ref[1].tolist()
         assert p_sum == ref[2].sum().item() and pi == ref[3].tolist() and names == ref[4]
+
+
+def _gather_to_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from aaclip.parallel import gather_rows_to
+    a, b = shard_range(n, rank, world)
+    local = torch.arange(a, b, dtype=torch.float32)[:, None, None].expand(-1, 3, 5).contiguous() * 0.25
+    res = {}
+    for staging in (False, True, None):  # False: the device-tensor (RCCL) branch, no host copy
+        out = gather_rows_to(local, n, dst=1, host_staging=staging)
+        res[str(staging)] = None if out is None else (list(out.shape), out[:, 0, 0].tolist(), str(out.device))
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [7, 8, 1])
+def test_gloo_world2_gather_rows_to_both_branches(n):
+    """gather_rows_to onto rank 1 through BOTH of its branches: the direct gather of the
+    tensor where it lives (the branch RCCL takes on the MI355X node; forced here with host
+    tensors over gloo) and the host-staged one (gloo rehearsals on cuda:0). Uneven (4 + 3),
+    even and one-empty-shard cases; only dst receives."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_to_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(v is None for v in out[0].values())
+    for v in out[1].values():
+        assert v == ([n, 3, 5], [i * 0.25 for i in range(n)], "cpu")

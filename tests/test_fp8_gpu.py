@@ -169,7 +169,10 @@ def test_quant_fp8_mx(dev, dtype, rows, cols):
     assert ((deq - xf).abs() <= 2.0 ** -4 * xf.abs() + step * 2.0 ** -9).all()
 
 
-@pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768 + 256, 1024), (300, 256, 128)])
+# K = 128 / 256 / 384: nk = 1, 2 (the steady-state loop runs zero times: the prologue hands
+# straight to the counted nk-2 tail) and 3 (odd) K-steps of 128
+@pytest.mark.parametrize("M,N,K", [(1154, 3072, 1024), (37, 1024, 4096), (577 * 3, 768 + 256, 1024), (300, 256, 128),
+                                   (4616, 4096, 256), (4616, 1024, 384), (300, 256, 256)])
 def test_gemm_fp8mx(dev, mx_variant, M, N, K):
     torch.manual_seed(M + N * 3 + K)
     a = torch.randn(M, K, device=dev) * torch.logspace(-2, 2, K // 64, device=dev).repeat_interleave(64)
@@ -243,11 +246,14 @@ def test_gemm_fp8mx_gelu_fp8_output_chain(dev, mx_variant, act):
     assert ((y.double() - y_ref).abs() <= 3e-5 * scale + 1e-6).all()
 
 
-def test_gemm_fp8mx_8ph_race_screen(dev):
+@pytest.mark.parametrize("K", [1024, 256, 384])
+def test_gemm_fp8mx_8ph_race_screen(dev, K):
     """The 8-phase MX kernel places its LDS hand-offs (tiles and the scale ring) by
-    vmcnt/barrier counting; repeated launches must be bit-identical."""
-    torch.manual_seed(5)
-    M, N, K = 577 * 8, 4096, 1024
+    vmcnt/barrier counting; repeated launches must be bit-identical. K = 256 / 384 screen
+    the counted tail (waits 9/9/9/4 then 2/0/0/0) where the steady-state loop runs zero
+    times or once."""
+    torch.manual_seed(5 + K)
+    M, N = 577 * 8, 4096
     a = torch.randn(M, K, device=dev) * torch.logspace(-1, 1, K // 64, device=dev).repeat_interleave(64)
     a8 = torch.empty(M, K, device=dev, dtype=FP8)
     asc = ops.mx_scales(M, K, dev)

@@ -682,3 +682,30 @@ def test_image_score_strided_rows(dev, dt, B, g, L):
     assert (d1.double() - ref_det).abs().max().item() < 1e-6
     ref_score = (ref_det @ T[:, 1].double() + 1) / 2
     assert (s1.double() - ref_score).abs().max().item() < 1e-6
+
+
+def test_tune_gemm_pins_an_accepted_family(dev):
+    """ops.tune_gemm (AACLIP_GEMM_TUNE=1 at workspace creation) measures every family in
+    GEMM_FAMILIES on one shape and pins the fastest; every family it tries must be one
+    aaclip_gemm_pin accepts (round 5 removed family 10 from the library but not from the
+    tuner, so the tuner raised on every block-GEMM shape). Pinning is bit-neutral."""
+    from aaclip import _lib
+    g = torch.Generator(device=dev).manual_seed(3)
+    M, N, K = 577 * 2, 1024, 1024
+    a = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).bfloat16()
+    res = torch.randn(M, N, device=dev, generator=g)
+    ref = res.clone()
+    ops.gemm(a, w, ref, residual=ref)
+    out = res.clone()
+    try:
+        fam = ops.tune_gemm(a, w, torch.empty_like(res), residual=torch.zeros_like(res))
+        assert fam in (0,) + ops.GEMM_FAMILIES
+        for f in ops.GEMM_FAMILIES:  # the tuner's whole list is pinnable
+            assert _lib.lib().aaclip_gemm_pin(_lib.BF16, 7, 1024, 1024, f) == 0
+            assert _lib.lib().aaclip_gemm_pin(_lib.BF16, 7, 1024, 1024, 0) == 0
+        ops.gemm(a, w, out, residual=out)
+        assert torch.equal(out, ref)
+    finally:
+        _lib.call("aaclip_gemm_pin", _lib.BF16, M, N, K, 0)
+        ops._tuned.pop((_lib.BF16, M, N, K), None)

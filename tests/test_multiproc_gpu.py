@@ -42,6 +42,35 @@ def test_bench_two_ranks_real_engine(dev):
     assert d["gather_verified"] and d["own_slice_verified"], d
     assert d["checked_shard"]["rank"] == 1 and d["checked_shard"]["images"] == [32, 64]
     assert line["step_outputs_verified"]["finite"] and line["step_outputs_verified"]["equal_to_one_stream_eager"]
+    assert line["parity_gate"] is True, line.get("parity_gate_failed")
+
+
+@pytest.mark.timeout(900)
+def test_bench_c3_partition_eight_ranks_real_engine(dev):
+    """Config C3's exact partition through the real engine: 8 ranks x 32 images = a global
+    batch of 256 (shard_range: rank r owns [32 r, 32 r + 32)), the per-step score
+    all-gather, max-over-ranks timing, the post-hoc self-check (rank 0 recomputes rank 7's
+    shard [224, 256) eagerly and compares bit for bit) and rank 0's timed-step check
+    against the CPU oracle with the parity gate. All 8 ranks share cuda:0 over gloo (RCCL
+    refuses two ranks on one device): a plumbing check of the N = 8 launch, not a scaling
+    number. Started as a fresh child process. Reference: test.py:53-99."""
+    env = dict(os.environ, AACLIP_BENCH_REHEARSAL="1", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "8", "--batch", "32", "--steps", "2",
+           "--warmup", "1", "--no-c5", "--no-modes", "--no-roofline", "--cpu-seconds", "0", "--streams", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=840)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    print({k: line[k] for k in ("value", "n_gpus", "ms_per_step")}, line["distributed"], line["timed_step_vs_oracle"])
+    assert line["n_gpus"] == 8
+    assert line["config"]["global_batch"] == 256 and line["config"]["per_gpu_batch"] == 32
+    d = line["distributed"]
+    assert d["world"] == 8 and d["backend"] == "gloo"
+    assert d["gather_verified"] and d["own_slice_verified"], d
+    assert d["checked_shard"] == {"rank": 7, "images": [224, 256], "checked_by": 0}
+    assert line["step_outputs_verified"]["finite"] and line["step_outputs_verified"]["equal_to_one_stream_eager"]
+    assert line["parity_gate"] is True and "timed_step_vs_oracle" in line["parity_gate_checked"]
 
 
 def _free_port():
