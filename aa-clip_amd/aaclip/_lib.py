@@ -10,7 +10,7 @@ import ctypes
 import os
 
 LIB_PATH = os.environ.get("AACLIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaaclip_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 F32 = 0
 BF16 = 1
@@ -36,6 +36,9 @@ SIGNATURES = {
     "aaclip_arch": [],
     "aaclip_trace_buffer": [_P, _P, ctypes.c_uint],
     "aaclip_gemm": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _I, _P, _P, _L, _P, _L, _I, _I, _I, _P],
+    "aaclip_gemm_ksplit_workspace": [_I, _I, _I, _I, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_L)],
+    "aaclip_gemm_ksplit": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _I, _P, _P, _L, _P, _L, _I, _P,
+                           ctypes.c_size_t, _P, _L, _P],
     "aaclip_gemm_fp8": [_I, _I, _I, _I, _P, _L, _P, _P, _L, _P, _P, _L, _I, _P, _P, _L, _P, _L, _I, _I, _I, _P],
     "aaclip_quant_fp8_rows": [_I, _P, _L, _P, _L, _P, _I, _I, _P],
     "aaclip_gemm_fp8mx": [_I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _P, _P, _L, _P, _L, _P, _L, _P],

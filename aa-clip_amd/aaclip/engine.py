@@ -42,6 +42,7 @@ DOMAIN_BLUR = {"Industrial": (7, 1.0), "Medical": (9, 1.5)}
 # (ops.tune_gemm) when AACLIP_GEMM_TUNE=1. Off by default: in the two-stream C2 pipeline the
 # isolated ranking does not carry over (tools/pin_search.py: the heuristic ~= the best pins)
 TUNE = os.environ.get("AACLIP_GEMM_TUNE", "0") == "1"
+CPROJ_KSPLIT = int(os.environ.get("AACLIP_CPROJ_KSPLIT", "0"))
 
 
 def _on_device(fn):
@@ -168,6 +169,10 @@ class VisualEngine:
         # AACLIP_MAP_PARTIALS=0 restores the row path (A/B). Captured graphs are keyed on it
         # (predict_cached).
         self.map_partials = os.environ.get("AACLIP_MAP_PARTIALS", "1") == "1"
+        # c_proj (K = 4096) as a fixed CPROJ_KSPLIT-way split-K GEMM in the 16-bit modes
+        # (aaclip_gemm_ksplit): the same split at every batch size, so per-image bits stay
+        # independent of the batch composition. 0 / 1 = unsplit.
+        self.cproj_ksplit = CPROJ_KSPLIT if (self.dtype != torch.float32 and not self.fp8) else 0
 
     # ------------------------------------------------------------------ workspace
     def _workspace(self, B: int, S: int, slot: int = 0):
@@ -209,6 +214,9 @@ class VisualEngine:
             asc=ops.mx_scales(R, WIDTH, dev) if self.fp8 else None,
             f8=e(R, 4 * WIDTH, dt=FP8) if self.fp8 else None,
             fsc=ops.mx_scales(R, 4 * WIDTH, dev) if self.fp8 else None,
+            # split-K c_proj: fp32 partial tiles + arrival counters (zeroed once; launches leave them zero)
+            kws=(ops.ksplit_workspace(R, WIDTH, 4 * WIDTH, self.cproj_ksplit, dev) if self.cproj_ksplit > 1
+                 else None),
             grid=e(B * P, dt=torch.float32), partial=e(B * ((P + 15) // 16) * EMBED, dt=torch.float32),
             det=e(B, EMBED, dt=torch.float32), score=e(B, dt=torch.float32),
             map=e(B, S, S, dt=torch.float32),
@@ -325,7 +333,8 @@ class VisualEngine:
                     return
                 ln2(blk, H)
                 ops.gemm(H, blk["w_fc"], ws["fc"], bias=blk["b_fc"], gelu=self.act)
-                ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=aux)
+                ops.gemm(ws["fc"], blk["w_pr"], X, bias=blk["b_pr"], residual=X, aux=aux, ksplit=self.cproj_ksplit,
+                         ksplit_ws=ws["kws"])
         for i in range(last):
             blk = self.blocks[i]
             qkv(blk)

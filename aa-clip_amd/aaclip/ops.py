@@ -82,12 +82,27 @@ def _rowmajor(t: torch.Tensor, name: str):
 
 
 # ------------------------------------------------------------------------ GEMM
+def ksplit_workspace(M: int, N: int, K: int, ksplit: int, device) -> tuple:
+    """(partials uint8 buffer, zeroed uint32 arrival counters) for aaclip_gemm_ksplit on
+    (M, N, K) split `ksplit` ways. One workspace per concurrently running launch."""
+    nbytes, ncnt = ctypes.c_size_t(0), ctypes.c_int64(0)
+    call("aaclip_gemm_ksplit_workspace", M, N, K, ksplit, ctypes.byref(nbytes), ctypes.byref(ncnt))
+    part = torch.empty(int(nbytes.value), device=device, dtype=torch.uint8)
+    cnt = torch.zeros(int(ncnt.value), device=device, dtype=torch.int32)
+    return part, cnt
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu=False, leaky=False,
-         residual=None, aux=None, row_group=0, row_group_out=0, row_offset=0) -> torch.Tensor:
+         residual=None, aux=None, row_group=0, row_group_out=0, row_offset=0, ksplit=0,
+         ksplit_ws=None) -> torch.Tensor:
     """out = epilogue(a @ w.T) — a [M,K], w [N,K] (same dtype), out [M', N].
     gelu: True = exact erf GELU (nn.GELU), "quick" = QuickGELU x*sigmoid(1.702x)
-    (reference model/transformer.py:46-49)."""
+    (reference model/transformer.py:46-49).
+    ksplit >= 2 (16-bit operands, no row remap): aaclip_gemm_ksplit, K cut into that many
+    fixed parts summed in index order, on ksplit_ws = ksplit_workspace(M, N, K, ksplit)."""
     _dev(a, w, out, bias, residual, aux)
+    if ksplit and ksplit > 1:
+        return _gemm_ksplit(a, w, out, bias, gelu, leaky, residual, aux, row_group, ksplit, ksplit_ws)
     for t, n in ((a, "a"), (w, "w"), (out, "out")):
         _rowmajor(t, n)
     if a.dtype != w.dtype:
@@ -109,6 +124,36 @@ def gemm(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu
             2.0 * M * N * K, nbytes, "aaclip_gemm", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w),
             w.stride(0), _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
             row_group, row_group_out, row_offset, _stream())
+    return out
+
+
+def _gemm_ksplit(a, w, out, bias, gelu, leaky, residual, aux, row_group, ksplit, ws):
+    for t, n in ((a, "a"), (w, "w"), (out, "out")):
+        _rowmajor(t, n)
+    if a.dtype not in (torch.bfloat16, torch.float16) or w.dtype != a.dtype:
+        raise TypeError("split-K gemm takes 16-bit operands of one dtype")
+    if out.dtype not in (torch.float32, a.dtype):
+        raise TypeError("gemm output must be float32 or the operands' 16-bit dtype")
+    if row_group:
+        raise ValueError("split-K gemm has no row remap")
+    if ws is None:
+        raise ValueError("split-K gemm needs its workspace (ops.ksplit_workspace)")
+    part, cnt = ws
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K or out.shape[1] != N or out.shape[0] < M:
+        raise ValueError(f"gemm shape mismatch a{tuple(a.shape)} w{tuple(w.shape)} out{tuple(out.shape)}")
+    _dev(part, cnt)
+    if part.dtype != torch.uint8 or cnt.dtype != torch.int32 or not (part.is_contiguous() and cnt.is_contiguous()):
+        raise TypeError("split-K workspace: (uint8 partials, int32 counters), contiguous")
+    epi, ldr, ldaux = _epilogue_flags(N, M, bias, gelu, leaky, residual, aux,
+                                      aux_dtype=torch.float16 if a.dtype == torch.float16 else torch.bfloat16)
+    kind = f"gemm N{N} K{K}" + (" leaky" if leaky else "") + (" qgelu" if gelu == "quick" else " gelu" if gelu else "") + (" resid" if residual is not None else "")
+    nbytes = (M * K + N * K) * a.element_size() + M * N * out.element_size() * (2 if residual is not None else 1)
+    _launch(kind, lambda: gemm_plan(dtag(a), M, N, K) + f" ksplit{ksplit}", 2.0 * M * N * K, nbytes,
+            "aaclip_gemm_ksplit", dtag(a), dtag(out), M, N, K, _ptr(a), a.stride(0), _ptr(w), w.stride(0),
+            _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux, ksplit,
+            _ptr(part), part.numel(), _ptr(cnt), cnt.numel(), _stream())
     return out
 
 

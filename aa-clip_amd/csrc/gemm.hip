@@ -51,6 +51,13 @@ struct GemmArgs {
   int64_t ld_cmx;
   const float* anchors;  // score-partials output (OUTM 3): text anchors T [t_period][2] (normal, abnormal)
   int t_period;          // column c uses anchor row c % t_period (the level width, 768)
+  // fixed split-K (aaclip_gemm_ksplit): every output tile is computed by `ksplit` workgroups,
+  // part h over K-steps [h nk / S, (h + 1) nk / S); each stores its fp32 partial tile to
+  // kpart, and the last to arrive (kcount[tile]) sums the S partials in index order and runs
+  // the epilogue. The split depends only on K, so the bits do not depend on M or the family.
+  int ksplit = 1;
+  float* kpart = nullptr;
+  unsigned* kcount = nullptr;
 };
 
 // out_dtype tag of the score-partials output (aaclip_gemm_scores; never a public dtype)
@@ -191,6 +198,94 @@ __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, i
   const int in_group = wgid % per_group;
   tm = first_m + in_group % gsize;
   tn = in_group / gsize;
+}
+
+// ---------------------------------------------------------------- fixed split-K
+// Workgroup -> (tile, part) for a split launch: the grid is 8 x ksplit x ceil(T/8) slots
+// (T = tiles). XCD x (= bid % 8, the hardware's round-robin) owns a contiguous run of tiles
+// (the bijective split of tile_coords) and its slots s = bid / 8 take part h = s % S of tile
+// s / S of that run: the S parts of a tile always share an XCD, so the L2 they meet in is
+// one cache (no agent-scope write-back / invalidate), and run back to back. Slots past the
+// XCD's run return false (nothing to do). Then the grouped tile order as in tile_coords.
+__device__ __forceinline__ bool split_coords(const GemmArgs& a, int bid, int& tm, int& tn, int& h) {
+  const int S = a.ksplit, T = a.tiles_m * a.tiles_n;
+  const int xcd = bid & 7, slot = bid >> 3;
+  const int q = T >> 3, r = T & 7;
+  const int run = q + (xcd < r ? 1 : 0);
+  const int lt = slot / S;
+  h = slot - lt * S;
+  if (lt >= run) return false;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + lt;
+  const int per_group = a.group_m * a.tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * a.group_m;
+  const int gsize = min(a.tiles_m - first_m, a.group_m);
+  const int in_group = wgid % per_group;
+  tm = first_m + in_group % gsize;
+  tn = in_group / gsize;
+  return true;
+}
+
+// K-steps [k0, k1) of part h of a fixed S-way split of nk steps
+__device__ __forceinline__ void split_range(int nk, int S, int h, int& k0, int& k1) {
+  k0 = (int)(((int64_t)h * nk) / S);
+  k1 = (int)(((int64_t)(h + 1) * nk) / S);
+}
+
+// After the main loop of a split launch (KS parts, a compile-time instantiation of its own,
+// so the unsplit kernels keep their registers): store this part's fp32 accumulators
+// (wave-linear, 1 KiB per wave instruction), count the arrival; every part but the last
+// returns false (no epilogue). The last one reloads the KS partials -- its own included,
+// so its accumulators are dead across the sum and their registers hold the loads -- and
+// sums them IN INDEX ORDER, ((P0 + P1) + P2) + ..., the same bits whichever part came
+// last; one accumulator row block's loads are in flight together (the memory clobber
+// between blocks keeps the compiler from hoisting every block's loads: scratch spills).
+// It resets the counter for the next launch and runs the epilogue. Arrival words carry
+// the XCC id (count in bits 0-7, sum of the parts' XCC ids from bit 8): parts that met
+// across XCDs (whose L2s are not coherent) would read stale partials, so that case
+// poisons the tile with NaN instead.
+template <int KS, int RM, int RN>
+__device__ __forceinline__ bool ksplit_combine(const GemmArgs& a, float4_t (&acc)[RM][RN], int tile, int h,
+                                               int nwaves, int wid, int lane, int* lds_flag) {
+  constexpr int PER_WAVE = RM * RN * 64;  // float4 per wave
+  const size_t part_f4 = (size_t)nwaves * PER_WAVE;
+  const float4_t* const base = (const float4_t*)a.kpart + (size_t)tile * KS * part_f4 + (size_t)wid * PER_WAVE + lane;
+  float4_t* const mine = (float4_t*)base + (size_t)h * part_f4;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) mine[(i * RN + j) * 64] = acc[i][j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has reached the L2
+  __syncthreads();                                   // ... and every wave's
+  if (threadIdx.x == 0) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const unsigned old = atomicAdd(a.kcount + tile, 1u + (xcc << 8));
+    const bool last = (int)(old & 0xff) == KS - 1;
+    if (last) a.kcount[tile] = 0u;  // ready for the next launch (kernel boundaries order it)
+    *lds_flag = last ? ((old >> 8) == (unsigned)(KS - 1) * xcc ? 1 : 2) : 0;
+  }
+  __syncthreads();
+  const int f = *lds_flag;
+  if (f == 0) return false;
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    asm volatile("" ::: "memory");
+    float4_t p[KS][RN];
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) p[q][j] = base[(size_t)q * part_f4 + (i * RN + j) * 64];
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      float4_t sum = p[0][j];
+#pragma unroll
+      for (int q = 1; q < KS; ++q) sum += p[q][j];
+      acc[i][j] = f == 1 ? sum : float4_t{NAN, NAN, NAN, NAN};
+    }
+  }
+  return true;
 }
 
 // Epilogue of one wave's (16*RM) x 64 output tile straight from the accumulators.
@@ -547,7 +642,7 @@ typedef __attribute__((ext_vector_type(4))) int i32x4_t;
 // e8m0 scale per (row, 64-K block) staged through LDS next to the tiles and applied
 // by the MFMA's B-operand scale (the A tile is the MFMA's second operand).
 // H16 (Q == 0 only): fp16 operands on v_mfma_f32_16x16x32_f16 (same tiles and cycles).
-template <int BM, int BN, int WM, int WN, int Q = 0, bool H16 = false>
+template <int BM, int BN, int WM, int WN, int Q = 0, bool H16 = false, int KS = 0>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   AACLIP_TRACE_SCOPE(TR_GEMM_TILE | gemm_trace_tag(a));
   static_assert(!H16 || Q == 0, "fp16 operands: 16-bit path only");
@@ -569,9 +664,20 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid / WN, wn = wid % WN;
 
-  int tm, tn;
-  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
+  static_assert(KS == 0 || !FP8, "split-K: 16-bit operands only");
+  int tm, tn, kh = 0;
+  if constexpr (KS > 1) {
+    if (!split_coords(a, blockIdx.x, tm, tn, kh)) return;  // a slot past this XCD's run of tiles
+  } else {
+    tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
+  }
   const int m0 = tm * BM, n0 = tn * BN;
+  int kb0 = 0, nk = a.K / BK;  // this part's K-steps [kb0, kb0 + nk)
+  if constexpr (KS > 1) {
+    int kb1;
+    split_range(nk, KS, kh, kb0, kb1);
+    nk = kb1 - kb0;
+  }
 
   const char* __restrict__ Ag = (const char*)a.A;
   const char* __restrict__ Wg = (const char*)a.W;
@@ -585,13 +691,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
     const int r = (i * NWAVES + wid) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (r & 7);
     const int gr = min(m0 + r, a.M - 1);
-    a_src[i] = Ag + ((size_t)gr * a.lda) * ES + c * 16;
+    a_src[i] = Ag + ((size_t)gr * a.lda) * ES + c * 16 + kb0 * 128;
   }
 #pragma unroll
   for (int i = 0; i < B_LOADS; ++i) {
     const int r = (i * NWAVES + wid) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (r & 7);
-    b_src[i] = Wg + ((size_t)(n0 + r) * a.ldw) * ES + c * 16;
+    b_src[i] = Wg + ((size_t)(n0 + r) * a.ldw) * ES + c * 16 + kb0 * 128;
   }
 
   // MX: the A tile's scales for K-step kt = BM rows x 2 bytes, contiguous in the
@@ -650,7 +756,6 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
     for (int kk = 0; kk < 2; ++kk) b_off[j][kk] = A_BYTES + r * 128 + ((chunk(kk) ^ (r & 7)) << 4);
   }
 
-  const int nk = a.K / BK;
   GEMM_STAGE(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
@@ -701,6 +806,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
+  }
+  if constexpr (KS > 1) {
+    if (!ksplit_combine<KS, RM, RN>(a, acc, tm * a.tiles_n + tn, kh, NWAVES, wid, lane, (int*)smem))
+      return;  // not the last part of this tile: its partial is stored
   }
   const int mw = m0 + wm * TM, nw = n0 + wn * TN;
   const int key = a.epi | (a.row_group > 0 ? EPI_REMAP : 0);
@@ -818,7 +927,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
 // step and was removed in round 5; it is in the round-4 history, family 5.)
 // SCORES: the instantiation for aaclip_gemm_scores (OUTM 3 epilogue only), so the
 // anomaly-map partials path adds no registers to the block-GEMM instantiations.
-template <bool H16, bool SCORES = false>
+#ifdef AACLIP_PHASE_STAMPS
+constexpr int kKsplitFlag = 2 * 4 * 128 * 128 + 1024 + 8 * 8 * 4 * 2 * 8;  // LDS byte offset of the split-K flag
+#else
+constexpr int kKsplitFlag = 2 * 4 * 128 * 128 + 1024;
+#endif
+
+template <bool H16, bool SCORES = false, int KS = 0>
 __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   AACLIP_TRACE_SCOPE(TR_GEMM_8PH | gemm_trace_tag(a));
   using V8 = h16x8_t<H16>;
@@ -842,10 +957,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   auto a_vo_of = [&](int m0) { return ((m0 + prow) * (int)a.lda + pchunk) * 2; };
   auto w_vo_of = [&](int n0) { return ((n0 + ((prow >> 5) & 1) * 64 + (prow & 31)) * (int)a.ldw + pchunk) * 2; };
   const int a_row = (int)a.lda * 2, w_row = (int)a.ldw * 2;  // bytes per row
-  const int nk = a.K / 64;
-  int tm, tn;
-  tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
-  const int avo = a_vo_of(tm * BM), wvo = w_vo_of(tn * BN);
+  int nk = a.K / 64;
+  static_assert(KS == 0 || !SCORES, "split-K: block GEMMs only");
+  int tm, tn, kh = 0, kb0 = 0;
+  if constexpr (KS > 1) {
+    if (!split_coords(a, blockIdx.x, tm, tn, kh)) return;  // a slot past this XCD's run of tiles
+    int kb1;
+    split_range(nk, KS, kh, kb0, kb1);
+    nk = kb1 - kb0;  // this part's K-steps [kb0, kb1): the operands' voffsets start at kb0
+  } else {
+    tile_coords(blockIdx.x, a.tiles_m, a.tiles_n, tm, tn, a.group_m);
+  }
+  const int avo = a_vo_of(tm * BM) + kb0 * 128, wvo = w_vo_of(tn * BN) + kb0 * 128;
   // region r of K-step kt into stage kt&1 (r: 0 = A0, 1 = A1, 2 = B0, 3 = B1)
   auto issue = [&](int r, int kt) {
     const int kc = kt * 128;
@@ -1006,6 +1129,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_8ph_kernel(GemmArgs a) {
   // both wave rows run the epilogue together (row 0 waits out row 1's last phase)
   if (wr == 0) __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");  // the epilogue's LDS slot writes stay behind that barrier
+  // split-K: the flag word sits past the ring and the staged bias (+16 B in launch_bf16_8ph)
+  if constexpr (KS > 1) {
+    if (!ksplit_combine<KS, RM, RN>(a, acc, tm * a.tiles_n + tn, kh, 8, wid, lane, (int*)(smem + kKsplitFlag)))
+      return;  // not the last part of this tile: its partial is stored
+  }
   const int mw = m0 + wr * TM, nw = n0 + wc * TN;
   const float* lbp = (const float*)(smem + 2 * STAGE) - n0;  // staged bias, by column
   // the epilogue's per-wave 4-KiB LDS slot: regions A1 / B1 of the last K-step's stage,
@@ -1265,20 +1393,45 @@ int launch_fp8mx_8ph(GemmArgs a, hipStream_t s) {
 
 int cu_count();
 
+// workgroups of a launch: one per tile, or 8 x ksplit x ceil(tiles / 8) slots for a split
+// launch (split_coords: each XCD's run of tiles, ksplit parts each; slots past a run idle)
+unsigned grid_of(const GemmArgs& a) {
+  const int64_t T = (int64_t)a.tiles_m * a.tiles_n;
+  return (unsigned)(a.ksplit > 1 ? 8 * a.ksplit * ((T + 7) / 8) : T);
+}
+
+template <bool H16, bool SCORES = false, int KS = 0>
+int launch_bf16_8ph_ks(GemmArgs a, hipStream_t s) {
+  // the ring + the tile's bias (+ the phase stamps in the diagnostic build) + the split-K flag
+  const size_t lds = kKsplitFlag + 16;
+  static unsigned attr_dev = 0;
+  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, SCORES, KS>, (int)lds, attr_dev))
+    return AACLIP_ERR_LAUNCH;
+  gemm_bf16_8ph_kernel<H16, SCORES, KS><<<grid_of(a), 512, lds, s>>>(a);
+  AACLIP_CHECK_LAUNCH();
+  return AACLIP_OK;
+}
+
 template <bool H16, bool SCORES = false>
 int launch_bf16_8ph(GemmArgs a, hipStream_t s) {
   if (a.N % 256 || a.K % 64) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, 256);
   a.tiles_n = a.N / 256;
-#ifdef AACLIP_PHASE_STAMPS
-  const size_t lds = 2 * 4 * 128 * 128 + 1024 + 8 * 8 * 4 * 2 * 8;  // + the phase stamps (diagnostic build)
-#else
-  const size_t lds = 2 * 4 * 128 * 128 + 1024;  // the ring + the tile's bias
-#endif
+  if constexpr (!SCORES) {
+    if (a.ksplit == 2) return launch_bf16_8ph_ks<H16, false, 2>(a, s);
+    if (a.ksplit == 3) return launch_bf16_8ph_ks<H16, false, 3>(a, s);
+    if (a.ksplit == 4) return launch_bf16_8ph_ks<H16, false, 4>(a, s);
+  }
+  return launch_bf16_8ph_ks<H16, SCORES, 0>(a, s);
+}
+
+template <int BM, int BN, int WM, int WN, int Q, bool H16, int KS>
+int launch_bf16_ks(GemmArgs a, hipStream_t s) {
+  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (Q == 2 ? 2 * BM * 2 : 0);
   static unsigned attr_dev = 0;
-  if (!lds_attr_once((const void*)gemm_bf16_8ph_kernel<H16, SCORES>, (int)lds, attr_dev))
+  if (!lds_attr_once((const void*)gemm_bf16_kernel<BM, BN, WM, WN, Q, H16, KS>, (int)lds, attr_dev))
     return AACLIP_ERR_LAUNCH;
-  gemm_bf16_8ph_kernel<H16, SCORES><<<a.tiles_m * a.tiles_n, 512, lds, s>>>(a);
+  gemm_bf16_kernel<BM, BN, WM, WN, Q, H16, KS><<<grid_of(a), WM * WN * 64, lds, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
 }
@@ -1288,13 +1441,12 @@ int launch_bf16(GemmArgs a, hipStream_t s) {
   if (a.N % BN) return AACLIP_ERR_ARG;
   a.tiles_m = ceil_div(a.M, BM);
   a.tiles_n = a.N / BN;
-  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (Q == 2 ? 2 * BM * 2 : 0);
-  static unsigned attr_dev = 0;
-  if (!lds_attr_once((const void*)gemm_bf16_kernel<BM, BN, WM, WN, Q, H16>, (int)lds, attr_dev))
-    return AACLIP_ERR_LAUNCH;
-  gemm_bf16_kernel<BM, BN, WM, WN, Q, H16><<<a.tiles_m * a.tiles_n, WM * WN * 64, lds, s>>>(a);
-  AACLIP_CHECK_LAUNCH();
-  return AACLIP_OK;
+  if constexpr (Q == 0) {
+    if (a.ksplit == 2) return launch_bf16_ks<BM, BN, WM, WN, Q, H16, 2>(a, s);
+    if (a.ksplit == 3) return launch_bf16_ks<BM, BN, WM, WN, Q, H16, 3>(a, s);
+    if (a.ksplit == 4) return launch_bf16_ks<BM, BN, WM, WN, Q, H16, 4>(a, s);
+  }
+  return launch_bf16_ks<BM, BN, WM, WN, Q, H16, 0>(a, s);
 }
 
 
@@ -1521,6 +1673,48 @@ extern "C" int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K, con
   gemm_f32_kernel<<<a.tiles_m * a.tiles_n, 256, 0, s>>>(a);
   AACLIP_CHECK_LAUNCH();
   return AACLIP_OK;
+}
+
+// Split-K workspace bound over every tile family the dispatch may pick for (M, N): S fp32
+// partial tiles per output tile (<= S (M + 319) N floats: 320-row tiles pad M the most) and
+// one arrival counter per tile (most tiles: 64x64).
+extern "C" int aaclip_gemm_ksplit_workspace(int M, int N, int K, int ksplit, size_t* part_bytes,
+                                            int64_t* counters) {
+  AACLIP_REQUIRE(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 64 == 0 && ksplit >= 2 && ksplit <= 4 &&
+                 ksplit <= K / 64 && part_bytes && counters);
+  *part_bytes = (size_t)ksplit * ((size_t)M + 319) * (size_t)N * 4;
+  *counters = (int64_t)ceil_div(M, 64) * (N / 64);
+  return AACLIP_OK;
+}
+
+extern "C" int aaclip_gemm_ksplit(int in_dtype, int out_dtype, int M, int N, int K, const void* A, int64_t lda,
+                                  const void* W, int64_t ldw, void* C, int64_t ldc, int epilogue, const float* bias,
+                                  const float* residual, int64_t ldr, void* aux, int64_t ldaux, int ksplit,
+                                  void* part, size_t part_bytes, void* counters, int64_t n_counters, void* stream) {
+  AACLIP_REQUIRE(in_dtype == AACLIP_BF16 || in_dtype == AACLIP_F16);
+  AACLIP_REQUIRE(out_dtype == AACLIP_F32 || out_dtype == in_dtype);
+  AACLIP_REQUIRE(A && W && C && M >= 0 && N > 0 && K > 0 && K % 64 == 0);
+  AACLIP_REQUIRE(lda >= K && ldw >= K && ldc >= N && lda % 8 == 0 && ldw % 8 == 0 && ldc % 4 == 0);
+  AACLIP_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0 && ((uintptr_t)C % 16) == 0);
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_BIAS) || (bias && ((uintptr_t)bias % 16) == 0));
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_RESID) || (residual && ldr >= N && ldr % 4 == 0));
+  AACLIP_REQUIRE(!(epilogue & AACLIP_EPI_AUX_BF16) || (aux && ldaux >= N && ldaux % 4 == 0));
+  AACLIP_REQUIRE((epilogue & ~63) == 0 && (epilogue & (AACLIP_EPI_GELU | AACLIP_EPI_QGELU)) !=
+                                               (AACLIP_EPI_GELU | AACLIP_EPI_QGELU));
+  AACLIP_REQUIRE(ksplit >= 2 && ksplit <= 4 && ksplit <= K / 64);
+  AACLIP_REQUIRE(part && counters && ((uintptr_t)part % 16) == 0 && ((uintptr_t)counters % 4) == 0);
+  if (M == 0) return AACLIP_OK;
+  size_t need_bytes = 0;
+  int64_t need_counters = 0;
+  if (aaclip_gemm_ksplit_workspace(M, N, K, ksplit, &need_bytes, &need_counters) != AACLIP_OK)
+    return AACLIP_ERR_ARG;
+  AACLIP_REQUIRE(part_bytes >= need_bytes && n_counters >= need_counters);
+  GemmArgs a{A, W, C, bias, residual, aux, lda, ldw, ldc, ldr, ldaux, M, N, K, epilogue,
+             out_dtype, 0, 0, 0, 0, 0, g_group_m, g_setprio, g_dbg & 2,
+             nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, ksplit, (float*)part, (unsigned*)counters};
+  hipStream_t s = (hipStream_t)stream;
+  if (in_dtype == AACLIP_BF16) return dispatch16<false>(a, s);
+  return dispatch16<true>(a, s);
 }
 
 extern "C" int aaclip_gemm_scores(int in_dtype, int M, int N, int K, const void* A, int64_t lda, const void* W,

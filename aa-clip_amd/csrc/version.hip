@@ -1,7 +1,7 @@
 // ABI version / target query (include/aaclip.h), and the diagnostic trace buffer.
 #include "common.h"
 
-extern "C" int aaclip_abi_version(void) { return 6; }
+extern "C" int aaclip_abi_version(void) { return 7; }
 extern "C" const char* aaclip_arch(void) { return "gfx950"; }
 
 #ifdef AACLIP_TRACE

@@ -92,6 +92,25 @@ int aaclip_gemm(int in_dtype, int out_dtype, int M, int N, int K,
                 int row_group, int row_group_out, int row_offset, void* stream);
 
 /*
+ * aaclip_gemm with a FIXED ksplit-way split of K (the MLP c_proj, K = 4096:
+ * model/transformer.py:216 / :257): every output tile is computed by `ksplit`
+ * workgroups, part h over K-steps [h*nk/ksplit, (h+1)*nk/ksplit) (nk = K/64), each
+ * storing its fp32 partial tile to `part`; the last part to arrive sums the partials
+ * in index order ((P0 + P1) + P2 ...) and runs the epilogue. The split depends only on
+ * K, so the bits do not depend on M, the batch composition or the tile family (every
+ * family splits alike) -- but they differ from the unsplit aaclip_gemm's. Fills the
+ * CUs that a launch with few K-long tiles leaves idle. 16-bit in_dtype only, no row
+ * remap; 2 <= ksplit <= min(4, K/64). Workspace: `part` >= part_bytes and `counters`
+ * (uint32, ZERO before first use; every launch leaves them zero) >= n_counters from
+ * aaclip_gemm_ksplit_workspace. Concurrent launches need separate workspaces.
+ */
+int aaclip_gemm_ksplit_workspace(int M, int N, int K, int ksplit, size_t* part_bytes, int64_t* n_counters);
+int aaclip_gemm_ksplit(int in_dtype, int out_dtype, int M, int N, int K, const void* A, int64_t lda,
+                       const void* W, int64_t ldw, void* C, int64_t ldc, int epilogue, const float* bias,
+                       const float* residual, int64_t ldr, void* aux, int64_t ldaux, int ksplit,
+                       void* part, size_t part_bytes, void* counters, int64_t n_counters, void* stream);
+
+/*
  * Level projection straight into anomaly-map partials (the predict path: the full
  * projected rows are never written):
  *   v = epilogue(A[M,K] . W[N,K]^T)   (epilogue 0 or AACLIP_EPI_LEAKY)

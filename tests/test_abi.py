@@ -176,3 +176,19 @@ def test_tuner_families_are_all_pinnable():
         assert lib.aaclip_gemm_pin(_lib.BF16, 1234, 1024, 1024, fam) == 0, fam
         assert lib.aaclip_gemm_pin(_lib.BF16, 1234, 1024, 1024, 0) == 0
     assert 10 not in ops.GEMM_FAMILIES and lib.aaclip_gemm_pin(_lib.BF16, 1234, 1024, 1024, 10) == 1
+
+
+def test_gemm_ksplit_argument_validation():
+    """aaclip_gemm_ksplit refuses what its grid and workspace cannot take (host logic)."""
+    lib = _lib.lib()
+    nb, nc = ctypes.c_size_t(0), ctypes.c_int64(0)
+    assert lib.aaclip_gemm_ksplit_workspace(9232, 1024, 4096, 3, ctypes.byref(nb), ctypes.byref(nc)) == 0
+    assert nb.value == 3 * (9232 + 319) * 1024 * 4 and nc.value == 145 * 16
+    assert lib.aaclip_gemm_ksplit_workspace(9232, 1024, 4096, 5, ctypes.byref(nb), ctypes.byref(nc)) == 1
+    assert lib.aaclip_gemm_ksplit_workspace(9232, 1024, 128, 3, ctypes.byref(nb), ctypes.byref(nc)) == 1  # 2 K-steps
+    f16 = ctypes.c_void_p(16)
+    args = [1, 0, 9232, 1024, 4096, f16, 4096, f16, 4096, f16, 1024, 0, None, None, 0, None, 0]
+    # workspace too small / split out of range / fp32 operands
+    assert lib.aaclip_gemm_ksplit(*args, 3, f16, 1024, f16, 10 ** 6, None) == 1
+    assert lib.aaclip_gemm_ksplit(*args, 1, f16, 10 ** 12, f16, 10 ** 6, None) == 1
+    assert lib.aaclip_gemm_ksplit(*([0] + args[1:]), 3, f16, 10 ** 12, f16, 10 ** 6, None) == 1

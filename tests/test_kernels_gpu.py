@@ -709,3 +709,75 @@ def test_tune_gemm_pins_an_accepted_family(dev):
     finally:
         _lib.call("aaclip_gemm_pin", _lib.BF16, M, N, K, 0)
         ops._tuned.pop((_lib.BF16, M, N, K), None)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("S", [2, 3, 4])
+def test_gemm_ksplit_bits_independent_of_family_and_batch(dev, dt, S):
+    """aaclip_gemm_ksplit (the c_proj, K = 4096): every tile family splits K the same way
+    (K-steps [h nk / S, (h+1) nk / S)) and the last part sums the partials in index order,
+    so the bits of a row depend on neither the family nor M (the rows of 1 image inside a
+    batch of 5 = the 1-image launch) -- the batch-composition invariance the engine needs.
+    Against float64 within bf16 / fp16 accuracy; every counter back at zero afterwards."""
+    K, N = 4096, 1024
+    g = torch.Generator(device=dev).manual_seed(S)
+    M = 577 * 5
+    a = torch.randn(M, K, device=dev, generator=g).to(dt)
+    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
+    bias = torch.randn(N, device=dev, generator=g)
+    res = torch.randn(M, N, device=dev, generator=g)
+    outs = []
+    for f in (0, 3, 8, 9, 11):
+        _lib.call("aaclip_set_gemm_variant", f)
+        try:
+            ws = ops.ksplit_workspace(M, N, K, S, dev)
+            x = res.clone()
+            xaux = torch.empty(M, N, device=dev, dtype=dt)
+            ops.gemm(a, w, x, bias=bias, residual=x, aux=xaux, ksplit=S, ksplit_ws=ws)
+            o16 = torch.empty(M, N, device=dev, dtype=dt)
+            ops.gemm(a, w, o16, bias=bias, ksplit=S, ksplit_ws=ws)
+            ws1 = ops.ksplit_workspace(577, N, K, S, dev)
+            x1 = res[:577].clone()
+            ops.gemm(a[:577], w, x1, bias=bias, residual=x1, ksplit=S, ksplit_ws=ws1)
+            torch.cuda.synchronize()
+            assert int(ws[1].abs().sum()) == 0 and int(ws1[1].abs().sum()) == 0, f
+        finally:
+            _lib.call("aaclip_set_gemm_variant", 0)
+        assert torch.isfinite(x).all(), f
+        assert torch.equal(x1, x[:577]), f  # one image alone = that image inside a batch
+        assert torch.equal(xaux.view(torch.int16), x.to(dt).view(torch.int16)), f
+        outs.append((x, o16))
+    ref = (a.double() @ w.double().T + bias.double()) + res.double()
+    assert ((outs[0][0].double() - ref).abs() <= 2e-2 * ref.abs() + 2e-2).all()
+    for x, o16 in outs[1:]:
+        assert torch.equal(x, outs[0][0])
+        assert torch.equal(o16.view(torch.int16), outs[0][1].view(torch.int16))
+    # the split is a different fp32 association than the unsplit GEMM: close, not equal
+    x0 = res.clone()
+    ops.gemm(a, w, x0, bias=bias, residual=x0)
+    assert ((x0 - outs[0][0]).abs() <= 1e-4 * x0.abs() + 1e-4).all()
+
+
+@pytest.mark.parametrize("S", [2, 3, 4])
+def test_gemm_ksplit_race_screen(dev, S):
+    """The split parts meet through stored partials and an arrival counter: the last part
+    must see every other part's partial. Many launches of a many-tile shape (C2's 16-image
+    chunk on the 8-phase kernel) must give the same bits every time and leave the counters
+    at zero."""
+    K, N, M = 4096, 1024, 9232
+    g = torch.Generator(device=dev).manual_seed(7 + S)
+    a = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, device=dev, generator=g)
+    res = torch.randn(M, N, device=dev, generator=g)
+    ws = ops.ksplit_workspace(M, N, K, S, dev)
+    first = res.clone()
+    ops.gemm(a, w, first, bias=bias, residual=first, ksplit=S, ksplit_ws=ws)
+    for _ in range(12):
+        x = res.clone()
+        ops.gemm(a, w, x, bias=bias, residual=x, ksplit=S, ksplit_ws=ws)
+        assert torch.equal(x, first)
+    torch.cuda.synchronize()
+    assert int(ws[1].abs().sum()) == 0
+    ref = (a.double() @ w.double().T + bias.double()) + res.double()
+    assert ((first.double() - ref).abs() <= 2e-2 * ref.abs() + 2e-2).all()

@@ -2,7 +2,9 @@
 in ONE process and timed in interleaved rounds. An arm is `name=N:K:fam,N:K:fam,...`: the
 chunk's block-GEMM shape (rows = the chunk's B*577, N, K) pinned to tile family `fam`
 (aaclip_gemm_pin; pins are read at launch, so each capture keeps its own). Same bits in
-every arm (every family accumulates K in the same order) -- checked against arm 0.
+every arm (every family accumulates K in the same order) -- checked against arm 0. An item
+`ksS` sets the engine's c_proj split-K (aaclip_gemm_ksplit, S parts; 0 = unsplit) for that arm
+(different bits from the unsplit arms: a different fp32 association).
 usage: python tools/step_arms.py base= outproj=1024:1024:8 nk1024=1024:1024:8,1024:4096:8
        [--img-size 448 --levels 4,8,12,16,20,24 --dtype bf16|fp8]  (config C5; fp8 pins only the bf16 GEMMs)"""
 import argparse
@@ -40,7 +42,9 @@ def main():
     runs = {}
     for arm in a.arms:
         name, _, spec = arm.partition("=")
-        pins = [tuple(int(v) for v in p.split(":")) for p in spec.split(",") if p]
+        items = [p for p in spec.split(",") if p]
+        eng.cproj_ksplit = next((int(p[2:]) for p in items if p.startswith("ks")), 0)
+        pins = [tuple(int(v) for v in p.split(":")) for p in items if not p.startswith("ks")]
         for n, k, fam in pins:
             _lib.call("aaclip_gemm_pin", _lib.BF16, rows, n, k, fam)
         runs[name] = eng.graphed_predict(B, S, "Industrial", streams=a.streams)  # dispatch baked in
