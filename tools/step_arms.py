@@ -4,7 +4,8 @@ chunk's block-GEMM shape (rows = the chunk's B*577, N, K) pinned to tile family 
 (aaclip_gemm_pin; pins are read at launch, so each capture keeps its own). Same bits in
 every arm (every family accumulates K in the same order) -- checked against arm 0. An item
 `ksS` sets the engine's c_proj split-K (aaclip_gemm_ksplit, S parts; 0 = unsplit) for that arm
-(different bits from the unsplit arms: a different fp32 association).
+(different bits from the unsplit arms: a different fp32 association); `avN` the attention
+variant (aaclip_set_attn_variant) captured into that arm.
 usage: python tools/step_arms.py base= outproj=1024:1024:8 nk1024=1024:1024:8,1024:4096:8
        [--img-size 448 --levels 4,8,12,16,20,24 --dtype bf16|fp8]  (config C5; fp8 pins only the bf16 GEMMs)"""
 import argparse
@@ -44,12 +45,14 @@ def main():
         name, _, spec = arm.partition("=")
         items = [p for p in spec.split(",") if p]
         eng.cproj_ksplit = next((int(p[2:]) for p in items if p.startswith("ks")), 0)
-        pins = [tuple(int(v) for v in p.split(":")) for p in items if not p.startswith("ks")]
+        _lib.call("aaclip_set_attn_variant", next((int(p[2:]) for p in items if p.startswith("av")), 0))
+        pins = [tuple(int(v) for v in p.split(":")) for p in items if not p[:2] in ("ks", "av")]
         for n, k, fam in pins:
             _lib.call("aaclip_gemm_pin", _lib.BF16, rows, n, k, fam)
         runs[name] = eng.graphed_predict(B, S, "Industrial", streams=a.streams)  # dispatch baked in
         for n, k, _ in pins:
             _lib.call("aaclip_gemm_pin", _lib.BF16, rows, n, k, 0)
+        _lib.call("aaclip_set_attn_variant", 0)
     ref = None
     for name, run in runs.items():
         m, s = run(x, T)
