@@ -190,27 +190,13 @@ __device__ __forceinline__ void attn_tile(const char* kt_lds, const h16x8_t<H16>
   }
 }
 
-// exp2 without the transcendental unit (A/B variants 4 / 5, the round-6 verdict's question):
-// Cody-Waite split x = n + f, n = rint(x), |f| <= 1/2, 2^f by a cubic (Taylor coefficients
-// of 2^f: relative error <= 6e-4, below bf16 / fp16 rounding of p), 2^n added into the
-// exponent field. x >= -125 keeps the exponent field positive (p is then ~2^-125, zero at
-// bf16 scale against the tile's 2^0..2^8). 7 single-issue VALU ops (max, rndne, sub, 3 fma,
-// cvt + lshl_add) against one v_exp_f32.
-__device__ __forceinline__ float exp2_emu(float x) {
-  x = fmaxf(x, -125.0f);
-  const float n = __builtin_rintf(x);
-  const float f = x - n;
-  const float p = fmaf(fmaf(fmaf(0.05550411f, f, 0.24022651f), f, 0.69314718f), f, 1.0f);
-  return __int_as_float(__float_as_int(p) + ((int)n << 23));
-}
-
 // Full 64-key tile for two 16-query blocks, phase-split: the same arithmetic as
 // attn_tile<4, 2, false>, ordered so each straight-line block pairs one block's
 // softmax VALU with the other block's MFMAs (Kᵀ·Q of block 1 beside the
 // exponentials of block 0, then P·V of block 0 beside the exponentials of block
 // 1). Each block's max-move branch sits between the two, before any of its p is
 // formed (the deferred-max rule of attn_tile).
-template <bool H16, int EMU = 0>
+template <bool H16>
 __device__ __forceinline__ void attn_tile_split(const char* kt_lds, const h16x8_t<H16> (&qf)[2][2],
                                                 float4_t (&ot)[2][4], float (&m_run)[2], float4_t (&l_acc)[2],
                                                 int g, int c, bool first) {
@@ -253,9 +239,9 @@ __device__ __forceinline__ void attn_tile_split(const char* kt_lds, const h16x8_
     for (int ks = 0; ks < 2; ++ks) {
       V8 v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {  // EMU of the 16 scores (indices 8 ks + i, 8 ks + 4 + i) emulated
-        v[i] = (E)(8 * ks + i < EMU ? exp2_emu(st[2 * ks][i]) : __builtin_amdgcn_exp2f(st[2 * ks][i]));
-        v[4 + i] = (E)(8 * ks + 4 + i < EMU ? exp2_emu(st[2 * ks + 1][i]) : __builtin_amdgcn_exp2f(st[2 * ks + 1][i]));
+      for (int i = 0; i < 4; ++i) {
+        v[i] = (E)__builtin_amdgcn_exp2f(st[2 * ks][i]);
+        v[4 + i] = (E)__builtin_amdgcn_exp2f(st[2 * ks + 1][i]);
       }
       pf[ks] = v;
     }
@@ -317,7 +303,7 @@ __device__ __forceinline__ void wait_barrier(bool deep) {
 // QB 16-query blocks per wave, NW waves per workgroup (QT = 16 * QB * NW queries),
 // NS-stage K/V ring. Every wave reads the whole K and V tile from LDS, so queries
 // per wave set the LDS bytes per FLOP: QB = 4 halves them against QB = 2.
-template <bool H16, int QB, int NW, int NS, int SPLIT, int EMU = 0>
+template <bool H16, int QB, int NW, int NS, int SPLIT>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_kernel(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int batch, int N, int H, int flags,
     uint8_t* __restrict__ out_mx, int64_t ld_mx) {
@@ -460,7 +446,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? ATTN_OCC : 4) void attn_bf16_ker
     const bool deep = advance();
     if (active) {
       if constexpr (SPLIT == 1 && QB == 2)
-        attn_tile_split<H16, EMU>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, g, c, t == 0);
+        attn_tile_split<H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, g, c, t == 0);
       else
         attn_tile<4, QB, false, H16>(smem + cur * (2 * KT * 128), qf, ot, m_run, l_acc, t * KT, q0, N, causal, g,
                                      c, t == 0);
@@ -756,26 +742,26 @@ __global__ __launch_bounds__(256, 2) void attn_f32_kernel(const float* __restric
 
 // 1 = 4 waves x 32 queries (3-stage ring, 3 workgroups per CU), 2 = 2 waves x 64
 // queries (2-stage ring, 4 workgroups per CU: half the LDS bytes per FLOP), 3 = 1
-// with the phase-split full tile (attn_tile_split: 3-6 % faster, the default), 4 / 5 = 3
-// with 4 / 8 of every 16 exponentials on the VALU (exp2_emu; A/B, round 6). Removed
-// in round 5 after measuring slower or equal (round-4 history): 4 = speculative
-// exponentials (same bits, equal), 5-7 = the 32x32x16 cross-tile pipelined kernel
-// (10 % slower at 2 workgroups per CU, spills at 3).
+// with the phase-split full tile (attn_tile_split: 3-6 % faster, the default). Removed
+// after measuring slower or equal: 4 = speculative exponentials (same bits, equal), 5-7 =
+// the 32x32x16 cross-tile pipelined kernel (10 % slower at 2 workgroups per CU, spills at
+// 3) in round 5 (round-4 history); in round 6, 4 / 5 = 4 / 8 of every 16 exponentials as
+// a Cody-Waite cubic on the VALU (-1.4 / -2.9 % in the step: profiles/r06/attn_exp_emulation_ab.txt).
 constexpr int kAttnDefault = 3;
 int g_attn_variant = 0;
 
-template <bool H16, int QB, int NW, int NS, int SPLIT = 0, int EMU = 0>
+template <bool H16, int QB, int NW, int NS, int SPLIT = 0>
 void launch_attn(const uint16_t* q, uint16_t* o, int batch, int seq, int heads, int flags, uint8_t* mx, int64_t ld_mx,
                  hipStream_t s) {
   const long nwg = (long)ceil_div(seq, 16 * QB * NW) * batch * heads;
-  attn_bf16_kernel<H16, QB, NW, NS, SPLIT, EMU>
+  attn_bf16_kernel<H16, QB, NW, NS, SPLIT>
       <<<(unsigned)nwg, 64 * NW, 0, s>>>(q, o, batch, seq, heads, flags, mx, ld_mx);
 }
 
 }  // namespace
 
 extern "C" int aaclip_set_attn_variant(int variant) {
-  AACLIP_REQUIRE(variant >= 0 && variant <= 5);
+  AACLIP_REQUIRE(variant >= 0 && variant <= 3);
   g_attn_variant = variant;
   return AACLIP_OK;
 }
@@ -800,14 +786,10 @@ extern "C" int aaclip_attention(int dtype, const void* qkv, void* out, int batch
     if (dtype == AACLIP_F16) {
       if (v == 2) launch_attn<true, 4, 2, 2>(q, o, batch, seq, heads, flags, nullptr, 0, s);
       else if (v == 3) launch_attn<true, 2, 4, ATTN_STAGES, 1>(q, o, batch, seq, heads, flags, nullptr, 0, s);
-      else if (v == 4) launch_attn<true, 2, 4, ATTN_STAGES, 1, 4>(q, o, batch, seq, heads, flags, nullptr, 0, s);
-      else if (v == 5) launch_attn<true, 2, 4, ATTN_STAGES, 1, 8>(q, o, batch, seq, heads, flags, nullptr, 0, s);
       else launch_attn<true, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, nullptr, 0, s);
     } else {
       if (v == 2) launch_attn<false, 4, 2, 2>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
       else if (v == 3) launch_attn<false, 2, 4, ATTN_STAGES, 1>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
-      else if (v == 4) launch_attn<false, 2, 4, ATTN_STAGES, 1, 4>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
-      else if (v == 5) launch_attn<false, 2, 4, ATTN_STAGES, 1, 8>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
       else launch_attn<false, 2, 4, ATTN_STAGES>(q, o, batch, seq, heads, flags, mx, ld_mx, s);
     }
   } else {

@@ -249,9 +249,7 @@ int aaclip_attention(int dtype, const void* qkv, void* out, int batch, int seq,
 
 /* Tuning hook for the 16-bit attention kernel: 0 = default (3), 1 = 4 waves x 32 queries per
  * workgroup, 2 = 2 waves x 64 queries, 3 = 1 with each full key tile phase-split so one
- * query block's softmax runs beside the other's MFMAs, 4 / 5 = 3 with 4 / 8 of every 16
- * exponentials computed on the VALU instead of v_exp_f32 (round-6 A/B). Process-global; for
- * benchmarking. */
+ * query block's softmax runs beside the other's MFMAs. Process-global; for benchmarking. */
 int aaclip_set_attn_variant(int variant);
 
 /*
