@@ -325,9 +325,12 @@ def gemm_fp8mx(a: torch.Tensor, a_sc: torch.Tensor, w: torch.Tensor, w_scale: to
     else:
         odt = dtag(out)
     epi, ldr, ldaux = _epilogue_flags(N, M, bias, gelu, leaky, residual, aux)
-    call("aaclip_gemm_fp8mx", odt, M, N, K, _ptr(a), a.stride(0), _ptr(a_sc), a_sc.shape[1], _ptr(w), w.stride(0),
-         _ptr(w_scale), _ptr(out), out.stride(0), epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux,
-         _ptr(out_sc), 0 if out_sc is None else out_sc.shape[1], _stream())
+    kind = f"gemm8 N{N} K{K}" + (" gelu" if gelu else "") + (" resid" if residual is not None else "")
+    nbytes = M * K + N * K + M * N * out.element_size() * (2 if residual is not None else 1)
+    _launch(kind, "gemm_fp8mx_8ph_kernel", 2.0 * M * N * K, nbytes, "aaclip_gemm_fp8mx", odt, M, N, K, _ptr(a),
+            a.stride(0), _ptr(a_sc), a_sc.shape[1], _ptr(w), w.stride(0), _ptr(w_scale), _ptr(out), out.stride(0),
+            epi, _ptr(bias), _ptr(residual), ldr, _ptr(aux), ldaux, _ptr(out_sc),
+            0 if out_sc is None else out_sc.shape[1], _stream())
     return out
 
 

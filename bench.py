@@ -290,7 +290,10 @@ class StepProbe:
 
 # op categories of the block GEMMs (ops.gemm's probe kind: N, K and epilogue)
 GEMM_OPS = {"gemm N3072 K1024": "qkv", "gemm N1024 K1024 resid": "out_proj", "gemm N4096 K1024 gelu": "c_fc",
-            "gemm N1024 K4096 resid": "c_proj", "gemm N1024 K1024 leaky": "adapter"}
+            "gemm N1024 K4096 resid": "c_proj", "gemm N1024 K1024 leaky": "adapter",
+            # fp8 MX block GEMMs (config C5's fp8 modes)
+            "gemm8 N3072 K1024": "qkv", "gemm8 N1024 K1024 resid": "out_proj", "gemm8 N4096 K1024 gelu": "c_fc",
+            "gemm8 N1024 K4096 resid": "c_proj"}
 
 
 def in_step_profile(eng, x, T, streams, replays=8):
