@@ -5,7 +5,8 @@ chunk's block-GEMM shape (rows = the chunk's B*577, N, K) pinned to tile family 
 every arm (every family accumulates K in the same order) -- checked against arm 0. An item
 `ksS` sets the engine's c_proj split-K (aaclip_gemm_ksplit, S parts; 0 = unsplit) for that arm
 (different bits from the unsplit arms: a different fp32 association); `avN` the attention
-variant (aaclip_set_attn_variant) captured into that arm.
+variant (aaclip_set_attn_variant), `gvN` the GEMM variant word (aaclip_set_gemm_variant: bits 4-7 =
+tile-order group height) captured into that arm.
 usage: python tools/step_arms.py base= outproj=1024:1024:8 nk1024=1024:1024:8,1024:4096:8
        [--img-size 448 --levels 4,8,12,16,20,24 --dtype bf16|fp8]  (config C5; fp8 pins only the bf16 GEMMs)"""
 import argparse
@@ -46,13 +47,15 @@ def main():
         items = [p for p in spec.split(",") if p]
         eng.cproj_ksplit = next((int(p[2:]) for p in items if p.startswith("ks")), 0)
         _lib.call("aaclip_set_attn_variant", next((int(p[2:]) for p in items if p.startswith("av")), 0))
-        pins = [tuple(int(v) for v in p.split(":")) for p in items if not p[:2] in ("ks", "av")]
+        _lib.call("aaclip_set_gemm_variant", next((int(p[2:]) for p in items if p.startswith("gv")), 0))
+        pins = [tuple(int(v) for v in p.split(":")) for p in items if not p[:2] in ("ks", "av", "gv")]
         for n, k, fam in pins:
             _lib.call("aaclip_gemm_pin", _lib.BF16, rows, n, k, fam)
         runs[name] = eng.graphed_predict(B, S, "Industrial", streams=a.streams)  # dispatch baked in
         for n, k, _ in pins:
             _lib.call("aaclip_gemm_pin", _lib.BF16, rows, n, k, 0)
         _lib.call("aaclip_set_attn_variant", 0)
+        _lib.call("aaclip_set_gemm_variant", 0)
     ref = None
     for name, run in runs.items():
         m, s = run(x, T)
