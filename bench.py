@@ -1019,14 +1019,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        # every rank's own elapsed time (load balance of the shards), then the MAX the line reports
+        t_all = torch.empty(world, device=dev, dtype=torch.float64)
+        dist.all_gather_into_tensor(t_all, torch.tensor([elapsed], device=dev, dtype=torch.float64))
+        per_rank = [round(v / args.steps * 1e3, 3) for v in t_all.tolist()]
+        elapsed = max(t_all.tolist())
         # the N-rank line proves its own result: own slices + a foreign shard recomputed
         # on rank 0 (eager, one stream: a different launch path from the timed graph)
         dist_check = verify_gather(lambda xi: eng.predict(xi, T, "Industrial", streams=1)[1].clone(), images_of,
                                    last[2], last[1], n_total)
+        dist_check["ms_per_step_per_rank"] = per_rank
     else:
         dist_check = None
 

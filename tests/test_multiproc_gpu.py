@@ -69,6 +69,7 @@ def test_bench_c3_partition_eight_ranks_real_engine(dev):
     assert d["world"] == 8 and d["backend"] == "gloo"
     assert d["gather_verified"] and d["own_slice_verified"], d
     assert d["checked_shard"] == {"rank": 7, "images": [224, 256], "checked_by": 0}
+    assert len(d["ms_per_step_per_rank"]) == 8 and max(d["ms_per_step_per_rank"]) == line["ms_per_step"]
     assert line["step_outputs_verified"]["finite"] and line["step_outputs_verified"]["equal_to_one_stream_eager"]
     assert line["parity_gate"] is True and "timed_step_vs_oracle" in line["parity_gate_checked"]
 
